@@ -1,0 +1,220 @@
+#!/usr/bin/env python
+"""Benchmark of the graphconvgeo hot path on MI355X: the GCN normalized-adjacency SpMM.
+
+Metric (BASELINE.json): "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph,
+1/2/4/8 GPU". One step = one forward SpMM Y = H . Z over the whole Twitter-World-scale
+synthetic graph (N = 1.4M users, E = 20M edges, nnz(H) = 2E + N, hidden K = 300, fp32),
+the S.dot(H, .) of mlpconv.py:73. Inputs are resident in HBM before the timed region.
+
+  value     = algorithmic bytes per step / step time (GB/s), bytes per SURVEY.md §8d:
+              B = 4(N+1) + 8 nnz + 4 K nnz + 4 K N
+  edges/s   = nnz(H) / step time
+  N > 1     : H row-partitioned (nnz-balanced) over N ranks, each step = RCCL all-gather of
+              Z over xGMI + local SpMM; total work fixed -> "strong" scaling.
+
+Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+from graphconvgeo_amd import sparse as gs  # noqa: E402
+from graphconvgeo_amd.synth import CONFIGS, SEED, synthetic_graph  # noqa: E402
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+
+def spmm_bytes(n_rows: int, nnz: int, K: int) -> int:
+    """Edge-centric algorithmic bytes of one CSR SpMM."""
+    return 4 * (n_rows + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n_rows
+
+
+def cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(H, K: int, budget_s: float) -> dict:
+    """The oracle (C port of scipy csr_matvecs, 1 thread) on a bounded row sample of the
+    same graph: consecutive row blocks of ~1M nonzeros until `budget_s` is spent."""
+    from oracle import gcn_oracle as O
+
+    rng = np.random.default_rng(SEED + 5)
+    Z = rng.standard_normal((H.shape[1], K), dtype=np.float32)
+    O.spmm_f32(H[:1000], Z)  # warm-up
+    rows_done = nnz_done = 0
+    t_total = 0.0
+    r = 0
+    n = H.shape[0]
+    while r < n and t_total < budget_s:
+        stop = int(np.searchsorted(H.indptr, H.indptr[r] + 1_000_000, side="left"))
+        stop = min(max(stop, r + 1), n)
+        blk = H[r:stop]
+        t0 = time.perf_counter()
+        O.spmm_f32(blk, Z)
+        t_total += time.perf_counter() - t0
+        rows_done += stop - r
+        nnz_done += blk.nnz
+        r = stop
+    gbs = spmm_bytes(rows_done, nnz_done, K) / t_total / 1e9
+    return {"value": round(gbs, 3), "unit": "GB/s", "cores": 1, "kind": "port",
+            "edges_per_s": round(nnz_done / t_total, 1),
+            "sample": f"rows [0, {rows_done}) of the same graph: {nnz_done} nnz x K={K} "
+                      f"in {t_total:.1f}s, oracle/spmm_oracle.c (scipy csr_matvecs port), "
+                      f"1 thread on {cpu_model()} ({os.cpu_count()} host cpus)"}
+
+
+def load_traffic(workload: str, per_launch_bytes: int):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload."""
+    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    if not os.path.exists(path):
+        return None, None
+    try:
+        with open(path) as f:
+            rec = json.load(f)
+        return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+    except (OSError, ValueError):
+        return None, None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", default="twitter-world", choices=sorted(CONFIGS))
+    ap.add_argument("--graph", default="powerlaw", choices=["powerlaw", "uniform"])
+    ap.add_argument("--hidden", type=int, default=None, help="K (default: config hidden=300)")
+    ap.add_argument("--mode", default="fast", choices=list(gs.MODES))
+    ap.add_argument("--task-nnz", type=int, default=0)
+    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    K = args.hidden or cfg.hidden
+    t_gen = time.perf_counter()
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=args.graph)
+    t_gen = time.perf_counter() - t_gen
+    N, nnz = H.shape[0], H.nnz
+    B = spmm_bytes(N, nnz, K)
+
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(SEED + rank)
+    if world == 1:
+        A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
+        Z = torch.randn((N, K), generator=gen, device=dev, dtype=torch.float32)
+        Y = gs.empty_dense(N, K, dev)
+        gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)  # builds the plan
+        info = A.plan(None, args.mode == "ordered", args.task_nnz).info() if args.mode != "rowwise" else {}
+
+        def step():
+            gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)
+    else:
+        from graphconvgeo_amd.distributed import RowPartitionedCSR
+        import torch.distributed as dist
+        part = RowPartitionedCSR(H, rank, world, dev)
+        Zl = torch.randn((part.block_rows, K), generator=gen, device=dev, dtype=torch.float32)
+        Y = gs.empty_dense(part.n_local, K, dev)
+        part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
+        info = part.A.plan(None, args.mode == "ordered", args.task_nnz).info() if args.mode != "rowwise" else {}
+
+        def step():
+            part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+        torch.cuda.synchronize(dev)
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms = elapsed / args.steps * 1e3
+
+    # Live per-launch kernel time with HIP events on the SpMM's own stream (N = 1 roofline).
+    roofline = None
+    if world == 1 and args.steps > 0:
+        stream = torch.cuda.current_stream(dev)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in range(args.steps)]
+        for a, b in evs:
+            a.record(stream)
+            step()
+            b.record(stream)
+        torch.cuda.synchronize(dev)
+        k_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        achieved = B / (k_ms * 1e-3) / 1e9
+        workload = f"{args.config}-{args.graph}-k{K}-{args.mode}"
+        traffic, traffic_src = load_traffic(workload, B)
+        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
+                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                    "traffic": traffic, "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
+                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": B}
+        if traffic_src:
+            roofline["traffic_source"] = traffic_src
+
+    value = B / (ms * 1e-3) / 1e9
+    rec = {
+        "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
+        "value": round(value, 1), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
+        "edges_per_s": round(nnz / (ms * 1e-3), 1),
+        "config": {"workload": f"{cfg.name} H.Z SpMM fwd, {args.graph} degrees", "nodes": N,
+                   "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": args.mode,
+                   "parallelism": f"row{world}" if world > 1 else "single",
+                   "plan": info, "graph_gen_s": round(t_gen, 1)},
+    }
+    if roofline:
+        rec["roofline"] = roofline
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        rec["cpu_baseline"] = cpu_baseline(H, K, args.cpu_budget)
+    if rank == 0:
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,98 @@
+"""ctypes binding of the C-ABI in include/gcg_spmm.h (libgcg_spmm.so).
+
+This is the same binding a maintainer would add on the reference side (see
+INTEGRATION.md): plain pointers and sizes, a hipStream_t, an int status. There is
+no fallback: if the library is missing or fails to load, every entry raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+from ._build import LIB
+
+GCG_OK = 0
+GCG_ACT_NONE = 0
+GCG_ACT_RELU = 1
+
+_STATUS_NAMES = {
+    0: "GCG_OK", 1: "GCG_ERR_INVALID_ARG", 2: "GCG_ERR_MISALIGNED", 3: "GCG_ERR_HIP",
+    4: "GCG_ERR_ALLOC", 5: "GCG_ERR_BAD_CSR", 6: "GCG_ERR_WORKSPACE",
+}
+
+_i64 = C.c_int64
+_p = C.c_void_p
+_pi64 = C.POINTER(C.c_int64)
+_psz = C.POINTER(C.c_size_t)
+
+# name -> (restype, argtypes); mirrors include/gcg_spmm.h one to one.
+SIGNATURES = {
+    "gcg_version": (C.c_char_p, []),
+    "gcg_last_error": (C.c_char_p, []),
+    "gcg_spmm_csr_f32": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
+                                   C.c_int, _p, _i64, _p]),
+    "gcg_spmm_plan_create": (C.c_int, [C.POINTER(_p), _i64, _i64, _i64, _p, _p, _i64, _i64,
+                                       C.c_int, _p]),
+    "gcg_spmm_plan_destroy": (C.c_int, [_p]),
+    "gcg_spmm_plan_workspace_bytes": (C.c_int, [_p, _i64, _psz]),
+    "gcg_spmm_plan_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
+    "gcg_spmm_csr_f32_planned": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
+                                           C.c_int, _p, C.c_size_t, _p]),
+    "gcg_spmm_plan_host": (C.c_int, [_i64, _p, _p, _i64, _i64, C.c_int, _p, _i64, _pi64, _p,
+                                     _i64, _pi64, _pi64]),
+    "gcg_csr_validate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p]),
+    "gcg_index_csr": (C.c_int, [_i64, _p, _i64, _p, _p, _p, C.c_size_t, _psz, _p]),
+    "gcg_scatter_add_rows_f32": (C.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p]),
+    "gcg_csr_transpose_f32": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p,
+                                        C.c_size_t, _psz, _p]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class NativeError(RuntimeError):
+    """A C-ABI call returned a non-zero gcg_status."""
+
+    def __init__(self, fn: str, status: int, msg: str):
+        self.status = status
+        super().__init__(f"{fn} -> {_STATUS_NAMES.get(status, status)}: {msg}")
+
+
+def lib_path() -> str:
+    return os.environ.get("GCG_LIB", LIB)
+
+
+def load() -> C.CDLL:
+    """Load libgcg_spmm.so (fail loudly; never fall back)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            path = lib_path()
+            if not os.path.exists(path):
+                raise ImportError(
+                    f"graphconvgeo_amd native library not found at {path}; run "
+                    "`python -m graphconvgeo_amd._build` (or __graft_entry__.build()) first")
+            lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+            for name, (res, args) in SIGNATURES.items():
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    """Call a status-returning entry point; raise NativeError on failure."""
+    lib = load()
+    st = getattr(lib, name)(*args)
+    if st != GCG_OK:
+        msg = lib.gcg_last_error().decode(errors="replace")
+        raise NativeError(name, st, msg)
+
+
+def version() -> str:
+    return load().gcg_version().decode()

@@ -1,0 +1,79 @@
+"""Host-side graph operator construction (reference layer L1, stays on the host).
+
+`normalize_adjacency` restates tensormain.py:168-181 (same computation at
+tensormain.py:94-106 and main.py:511-522):
+
+    adj = nx.adjacency_matrix(graph, nodelist=range(N), weight='w')   # binary: the
+          # projection at data.py:240-249 adds edges without a 'w' attribute
+    adj.setdiag(1)
+    d = adj.sum(axis=1);  d^-1/2 with inf -> 0
+    H = D^-1/2 * adj * D^-1/2           (float64, then .astype(float32), tensormain.py:221)
+
+`csr_from_edges` is the same operator built directly from an undirected edge list
+(what the synthetic benchmark graphs use): identical values, canonical (sorted)
+storage order.
+"""
+from __future__ import annotations
+
+import numpy as np
+import scipy.sparse as sps
+
+
+def normalize_csr(adj, dtype=np.float32) -> sps.csr_matrix:
+    """H = D^-1/2 (A + I) D^-1/2 from a (binary) adjacency, scipy expression order.
+
+    Mirrors tensormain.py:172-180 with the two fixes modern scipy needs:
+    `sp.sqrt/sp.isinf/sp.errstate` are numpy functions, and the product is spelled
+    with csr_matrix operands so `*` is a matrix product.
+    """
+    import warnings
+
+    adj = sps.csr_matrix(adj, copy=True)
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore", sps.SparseEfficiencyWarning)
+        adj.setdiag(1)
+    n, m = adj.shape
+    diags = np.asarray(adj.sum(axis=1)).flatten()
+    with np.errstate(divide="ignore"):
+        diags_sqrt = 1.0 / np.sqrt(diags)
+    diags_sqrt[np.isinf(diags_sqrt)] = 0
+    d = sps.spdiags(diags_sqrt, [0], m, n, format="csr")
+    h = d * adj * d
+    return sps.csr_matrix(h.astype(np.float64)).astype(dtype)
+
+
+def normalize_adjacency(graph, n_nodes: int, dtype=np.float32) -> sps.csr_matrix:
+    """tensormain.py:170-181 for a networkx graph over nodes 0..n_nodes-1."""
+    import networkx as nx
+
+    adj = nx.adjacency_matrix(graph, nodelist=range(n_nodes), weight="w")
+    return normalize_csr(adj, dtype=dtype)
+
+
+def csr_from_edges(n: int, u: np.ndarray, v: np.ndarray, dtype=np.float32,
+                   self_loops: bool = True) -> sps.csr_matrix:
+    """Symmetric normalized operator from undirected edges (u[i], v[i]), u != v, unique.
+
+    Values are 1/sqrt(d_i) * 1/sqrt(d_j) computed in float64 (d = degree + 1 with the
+    self loop, as setdiag(1) gives) and rounded once to `dtype`, exactly the entries the
+    reference's float64 D*A*D product holds before `.astype(float32)`.
+    Indices are sorted within each row; nnz = 2E + N.
+    """
+    u = np.asarray(u, dtype=np.int64)
+    v = np.asarray(v, dtype=np.int64)
+    rows = np.concatenate([u, v] + ([np.arange(n, dtype=np.int64)] if self_loops else []))
+    cols = np.concatenate([v, u] + ([np.arange(n, dtype=np.int64)] if self_loops else []))
+    key = rows * n + cols
+    order = np.argsort(key, kind="stable")
+    rows = rows[order]
+    cols = cols[order]
+    counts = np.bincount(rows, minlength=n)
+    indptr = np.zeros(n + 1, dtype=np.int64)
+    np.cumsum(counts, out=indptr[1:])
+    deg = counts.astype(np.float64)
+    with np.errstate(divide="ignore"):
+        dinv = 1.0 / np.sqrt(deg)
+    dinv[np.isinf(dinv)] = 0
+    data = (dinv[rows] * dinv[cols]).astype(dtype)
+    idx_t = np.int32 if (n < 2**31 and len(cols) < 2**31) else np.int64
+    return sps.csr_matrix((data, cols.astype(idx_t), indptr.astype(idx_t)), shape=(n, n))

@@ -1,0 +1,236 @@
+"""Graph-convolution layers with the reference's Lasagne plugin signatures (mlpconv.py:59-95).
+
+Reference (Lasagne `Layer` subclasses, Theano graph, host CPU):
+
+    SparseConvolutionDenseLayer(incoming, H=None, num_units, W=GlorotUniform(),
+                                b=Constant(0.), nonlinearity=rectify)          mlpconv.py:59-77
+        get_output_for(X) = nonlinearity(S.dot(H, S.dot(X, W)) + b);  X must be sparse
+    ConvolutionDenseLayer(incoming, H=None, num_units, nonlinearity=softmax)   mlpconv.py:79-95
+        get_output_for(h, target_indices=idx) = nonlinearity((S.dot(H, T.dot(h, W)) + b)[idx])
+
+Here: torch modules with the same constructor arguments and `get_output_for` /
+`forward(input, target_indices=None)`. The sparse products run in the HIP kernels
+(graphconvgeo_amd.sparse.spmm) with bias + rectify + the target-row subset fused in the
+epilogue; the dense projection T.dot(h, W) is a plain fp32 GEMM (torch.matmul ->
+hipBLASLt/rocBLAS on the f32 MFMA path). Backward follows Theano's rules: grad of
+S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H for the symmetric H; CSR(X^T) built once on the
+device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
+
+`GraphConvLayer` is the name BASELINE.json's north_star uses; it is the generic form.
+Differences from Theano, by design: at a pre-activation of exactly 0.0 Theano's relu
+gradient is 0.5*g (d/dx 0.5(x+|x|)); here it is 0 (the mask is output > 0).
+"""
+from __future__ import annotations
+
+from typing import Optional, Union
+
+import numpy as np
+import scipy.sparse as sps
+import torch
+import torch.nn as nn
+
+from . import sparse as gs
+
+_FUSED_ACTS = {"rectify": "relu", "relu": "relu"}
+
+
+def _glorot_uniform(fan_in: int, fan_out: int, generator=None) -> torch.Tensor:
+    """lasagne.init.GlorotUniform(gain=1.0) for a DenseLayer W of shape (num_inputs, num_units)."""
+    a = float(np.sqrt(6.0 / (fan_in + fan_out)))
+    return (torch.rand((fan_in, fan_out), generator=generator, dtype=torch.float32) * 2 - 1) * a
+
+
+def _as_tensor(x, shape, device) -> torch.Tensor:
+    t = torch.as_tensor(np.asarray(x, dtype=np.float32) if not isinstance(x, torch.Tensor) else x,
+                        dtype=torch.float32)
+    if tuple(t.shape) != tuple(shape):
+        raise ValueError(f"expected parameter of shape {shape}, got {tuple(t.shape)}")
+    return t.to(device).contiguous()
+
+
+def _num_inputs(incoming) -> int:
+    if isinstance(incoming, int):
+        return incoming
+    if isinstance(incoming, (tuple, list)):
+        return int(incoming[-1])
+    if hasattr(incoming, "num_units"):
+        return int(incoming.num_units)
+    raise ValueError("incoming must be an int (num inputs), a shape tuple or a layer")
+
+
+def _as_device_csr(m, device) -> gs.DeviceCSR:
+    if isinstance(m, gs.DeviceCSR):
+        return m
+    if sps.issparse(m):
+        return gs.DeviceCSR.from_scipy(m, device)
+    raise ValueError("Input for this layer must be sparse")
+
+
+class _CSRMatMul(torch.autograd.Function):
+    """Y = act(A . Z + bias)[rows]; differentiable in Z and bias (S.dot + epilogue)."""
+
+    @staticmethod
+    def forward(ctx, Z, bias, A: gs.DeviceCSR, act, rows, mode):
+        Y = gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
+        ctx.A, ctx.act, ctx.rows, ctx.mode = A, act, rows, mode
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(Y if act == "relu" else None)
+        return Y
+
+    @staticmethod
+    def backward(ctx, gY):
+        A, rows = ctx.A, ctx.rows
+        (Y,) = ctx.saved_tensors
+        g = gY if Y is None else gY * (Y > 0).to(gY.dtype)
+        g_bias = g.sum(dim=0) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        g_Z = None
+        if ctx.needs_input_grad[0]:
+            if rows is not None:
+                full = torch.zeros((A.n_rows, g.shape[1]), dtype=torch.float32, device=g.device)
+                seg_ptr, pos = _index_csr_cached(rows, A.n_rows)
+                gs.scatter_add_rows(full, seg_ptr, pos, g.contiguous())
+                g = full
+            g_Z = gs.spmm(A.transpose(), g.contiguous(), mode=ctx.mode)
+        return g_Z, g_bias, None, None, None, None
+
+
+def _index_csr_cached(rows: gs.RowSelection, n_rows: int):
+    cache = rows.__dict__.setdefault("_index_csr", {})
+    if n_rows not in cache:
+        cache[n_rows] = gs.index_csr(rows.device_rows, n_rows)
+    return cache[n_rows]
+
+
+def csr_matmul(A: gs.DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
+               act: Optional[str] = None, rows: Optional[gs.RowSelection] = None,
+               mode: str = "fast") -> torch.Tensor:
+    """Differentiable S.dot(A, Z) (+ bias, rectify, row subset) through the HIP kernels."""
+    return _CSRMatMul.apply(Z, bias, A, act, rows, mode)
+
+
+def _resolve_nonlinearity(nl):
+    """Returns (fused kernel activation or None, post-op callable or None)."""
+    if nl is None or nl in ("linear", "identity"):
+        return None, None
+    if isinstance(nl, str):
+        if nl in _FUSED_ACTS:
+            return _FUSED_ACTS[nl], None
+        if nl == "softmax":
+            return None, lambda x: torch.softmax(x, dim=1)
+        if nl == "tanh":
+            return None, torch.tanh
+        if nl == "sigmoid":
+            return None, torch.sigmoid
+        raise ValueError(f"unknown nonlinearity {nl!r}")
+    if nl is torch.relu or nl is torch.nn.functional.relu:
+        return "relu", None
+    return None, nl
+
+
+class GraphConvLayer(nn.Module):
+    """nonlinearity((H . (input . W) + b)[target_indices]) -- one graph-convolution layer.
+
+    input: sparse (scipy / DeviceCSR; X . W runs in the HIP SpMM) or dense torch tensor
+    (X . W is an fp32 GEMM). H: scipy sparse or DeviceCSR, uploaded once and shared.
+    """
+
+    def __init__(self, incoming=None, H=None, num_units: int = None, W=None, b=0.0,
+                 nonlinearity="rectify", device: Union[str, torch.device] = "cuda",
+                 mode: str = "fast", require_sparse_input: bool = False, generator=None,
+                 in_features: Optional[int] = None):
+        super().__init__()
+        if num_units is None:
+            raise ValueError("num_units is required")
+        if H is None:
+            raise ValueError("H (the normalized adjacency) is required")
+        self.device = torch.device(device)
+        self.num_inputs = in_features if in_features is not None else _num_inputs(incoming)
+        self.num_units = int(num_units)
+        self.H = _as_device_csr(H, self.device)
+        if self.H.symmetric is None:
+            self.H.symmetric = False  # transpose built on demand unless declared symmetric
+        w = _glorot_uniform(self.num_inputs, self.num_units, generator) if W is None else W
+        self.W = nn.Parameter(_as_tensor(w, (self.num_inputs, self.num_units), self.device))
+        if b is None:
+            self.b = None
+        else:
+            bb = np.full(self.num_units, float(b), np.float32) if np.isscalar(b) else b
+            self.b = nn.Parameter(_as_tensor(bb, (self.num_units,), self.device))
+        self.fused_act, self.post = _resolve_nonlinearity(nonlinearity)
+        self.mode = mode
+        self.require_sparse_input = require_sparse_input
+        self._sparse_inputs = {}
+
+    def _sparse_input(self, x) -> gs.DeviceCSR:
+        if isinstance(x, gs.DeviceCSR):
+            return x
+        key = (id(x), x.shape, x.nnz)
+        if key not in self._sparse_inputs:
+            self._sparse_inputs = {key: gs.DeviceCSR.from_scipy(x, self.device)}
+        return self._sparse_inputs[key]
+
+    def forward(self, input, target_indices=None, **kwargs):
+        is_sparse = isinstance(input, gs.DeviceCSR) or sps.issparse(input)
+        if self.require_sparse_input and not is_sparse:
+            raise ValueError("Input for this layer must be sparse")  # mlpconv.py:67-69
+        if is_sparse:
+            Z = csr_matmul(self._sparse_input(input), self.W, mode=self.mode)  # S.dot(X, W)
+        else:
+            Z = torch.matmul(input, self.W)  # T.dot(h, W), mlpconv.py:88
+        rows = None
+        if target_indices is not None:
+            rows = target_indices if isinstance(target_indices, gs.RowSelection) else \
+                gs.RowSelection(target_indices, self.device)
+        Y = csr_matmul(self.H, Z, self.b, self.fused_act, rows, self.mode)
+        return self.post(Y) if self.post is not None else Y
+
+    # Lasagne-style API
+    def get_output_for(self, input, **kwargs):
+        return self.forward(input, **kwargs)
+
+    def get_params(self):
+        return [p for p in (self.W, self.b) if p is not None]
+
+
+class SparseConvolutionDenseLayer(GraphConvLayer):
+    """mlpconv.py:59-77: nonlinearity(S.dot(H, S.dot(X, W)) + b); X must be sparse."""
+
+    def __init__(self, incoming=None, H=None, num_units=None, W=None, b=0.0,
+                 nonlinearity="rectify", **kw):
+        super().__init__(incoming, H=H, num_units=num_units, W=W, b=b,
+                         nonlinearity=nonlinearity, require_sparse_input=True, **kw)
+
+
+class ConvolutionDenseLayer(GraphConvLayer):
+    """mlpconv.py:79-95: nonlinearity((S.dot(H, T.dot(h, W)) + b)[target_indices])."""
+
+    def __init__(self, incoming=None, H=None, num_units=None, W=None, b=0.0,
+                 nonlinearity="softmax", **kw):
+        super().__init__(incoming, H=H, num_units=num_units, W=W, b=b,
+                         nonlinearity=nonlinearity, **kw)
+
+
+class GCN(nn.Module):
+    """The 2-layer model MLPCONV.fit builds (mlpconv.py:196-217), inputs resident in HBM.
+
+    forward(target_indices) -> softmax probabilities of the target rows.
+    """
+
+    def __init__(self, H, X, in_features: int, hidden: int, n_classes: int,
+                 device="cuda", W1=None, W2=None, mode: str = "fast", generator=None):
+        super().__init__()
+        self.device = torch.device(device)
+        Hd = _as_device_csr(H, self.device)
+        if Hd.symmetric is None:
+            Hd.symmetric = True  # D^-1/2 (A+I) D^-1/2 of an undirected graph (tensormain.py:170-180)
+        self.X = _as_device_csr(X, self.device)
+        self.l_hid1 = SparseConvolutionDenseLayer(in_features, H=Hd, num_units=hidden, W=W1,
+                                                  nonlinearity="rectify", device=self.device,
+                                                  mode=mode, generator=generator)
+        self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=n_classes,
+                                           W=W2, nonlinearity="softmax", device=self.device,
+                                           mode=mode, generator=generator)
+
+    def forward(self, target_indices):
+        h = self.l_hid1(self.X)
+        return self.l_out(h, target_indices=target_indices)

@@ -1,0 +1,326 @@
+"""HBM-resident CSR operators and the SpMM entry point (host mirror of `S.dot`).
+
+`DeviceCSR` holds a scipy-layout CSR (indptr/indices int32, data float32) in HBM.
+The reference keeps H as one host scipy matrix shared by both layers
+(`H=l_hid1.H`, mlpconv.py:214); here it is uploaded once and every layer, epoch
+and width K reuses the same device buffers and launch plans.
+
+`spmm(A, Z, ...)` is `theano.sparse.dot(A, Z)` (mlpconv.py:71,73,90) with the
+layer epilogue fused (bias, rectify, target-row subset). It always runs the HIP
+kernels in libgcg_spmm.so; there is no CPU path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import hashlib
+from typing import Optional, Union
+
+import numpy as np
+import scipy.sparse as sps
+import torch
+
+from . import _native
+from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call
+
+ACTS = {None: GCG_ACT_NONE, "none": GCG_ACT_NONE, "linear": GCG_ACT_NONE,
+        "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}
+
+MODES = ("fast", "ordered", "rowwise")
+
+
+def _stream_handle(device: torch.device) -> C.c_void_p:
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _require_cuda(t: torch.Tensor, name: str):
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a CUDA (HIP) tensor; the graphconvgeo_amd path has "
+                         "no CPU fallback")
+
+
+class RowSelection:
+    """A fixed list of output rows (the reference's `target_indices`, mlpconv.py:94).
+
+    Keeps the indices resident as int32 in HBM and carries a content key so the
+    launch plan built for it can be cached on the operator.
+    """
+
+    def __init__(self, rows, device: Union[str, torch.device] = "cuda"):
+        host = np.ascontiguousarray(np.asarray(rows).reshape(-1)).astype(np.int32, copy=False)
+        self.host = host
+        self.n = int(host.size)
+        self.key = hashlib.blake2b(host.tobytes(), digest_size=16).hexdigest() + f":{self.n}"
+        self.device_rows = torch.from_numpy(host).to(device)
+
+    def __len__(self):
+        return self.n
+
+
+class Plan:
+    """Owning wrapper of a gcg_spmm_plan (nnz-balanced task list for one CSR + rows)."""
+
+    def __init__(self, A: "DeviceCSR", rows: Optional[RowSelection], ordered: bool,
+                 task_nnz: int):
+        self.A = A
+        self.rows = rows
+        self.ordered = bool(ordered)
+        self.handle = C.c_void_p()
+        n_out = rows.n if rows is not None else A.n_rows
+        with torch.cuda.device(A.device):
+            call("gcg_spmm_plan_create", C.byref(self.handle), A.n_rows, A.n_cols, A.nnz,
+                 _ptr(A.indptr), _ptr(rows.device_rows) if rows is not None else None, n_out,
+                 int(task_nnz), int(ordered), _stream_handle(A.device))
+        self.n_out = n_out
+        self._ws = {}
+
+    def info(self) -> dict:
+        a, b, c, d = (C.c_int64() for _ in range(4))
+        call("gcg_spmm_plan_info", self.handle, C.byref(a), C.byref(b), C.byref(c), C.byref(d))
+        return {"n_tasks": a.value, "n_long_rows": b.value, "n_segments": c.value,
+                "max_task_nnz": d.value}
+
+    def workspace(self, K: int) -> Optional[torch.Tensor]:
+        nb = C.c_size_t()
+        call("gcg_spmm_plan_workspace_bytes", self.handle, int(K), C.byref(nb))
+        if nb.value == 0:
+            return None
+        ws = self._ws.get(K)
+        if ws is None:
+            ws = torch.empty((nb.value + 15) // 16 * 4, dtype=torch.float32, device=self.A.device)
+            self._ws[K] = ws
+        return ws
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h is not None and h.value:
+            try:
+                _native.load().gcg_spmm_plan_destroy(h)
+            except Exception:  # interpreter shutdown
+                pass
+            self.handle = None
+
+
+class DeviceCSR:
+    """CSR matrix (scipy layout: int32 indptr/indices, float32 data) resident in HBM."""
+
+    def __init__(self, indptr: torch.Tensor, indices: torch.Tensor, data: torch.Tensor,
+                 shape, symmetric: Optional[bool] = None, validate: bool = True):
+        for t, n in ((indptr, "indptr"), (indices, "indices"), (data, "data")):
+            _require_cuda(t, n)
+        if indptr.dtype != torch.int32 or indices.dtype != torch.int32:
+            raise TypeError("indptr/indices must be int32 (scipy layout for nnz < 2**31)")
+        if data.dtype != torch.float32:
+            raise TypeError("data must be float32 (mlpconv.py dtype='float32')")
+        self.indptr = indptr.contiguous()
+        self.indices = indices.contiguous()
+        self.data = data.contiguous()
+        self.shape = (int(shape[0]), int(shape[1]))
+        self.n_rows, self.n_cols = self.shape
+        self.nnz = int(self.indices.numel())
+        if self.indptr.numel() != self.n_rows + 1 or self.data.numel() != self.nnz:
+            raise ValueError("inconsistent CSR arrays")
+        self.device = self.indptr.device
+        self.symmetric = symmetric
+        self._plans = {}
+        self._transpose = None
+        if validate:
+            self.validate()
+
+    # -- construction -------------------------------------------------------------------
+    @classmethod
+    def from_scipy(cls, m, device: Union[str, torch.device] = "cuda",
+                   symmetric: Optional[bool] = None, check_symmetric: bool = False,
+                   validate: bool = True) -> "DeviceCSR":
+        """Upload a scipy sparse matrix, preserving its storage order (it defines the
+        accumulation order and hence the bitwise result, like scipy's csr_matvecs)."""
+        if not sps.issparse(m):
+            raise ValueError("Input for this layer must be sparse")
+        m = m.tocsr() if m.format != "csr" else m
+        if m.nnz >= 2**31 or m.shape[0] >= 2**31 - 1:
+            raise ValueError("CSR too large for int32 indices")
+        dev = torch.device(device)
+        if dev.type != "cuda":
+            raise ValueError("DeviceCSR lives in HBM: device must be a CUDA (HIP) device")
+        if check_symmetric and symmetric is None:
+            symmetric = m.shape[0] == m.shape[1] and (abs(m - m.T) > 0).nnz == 0
+        indptr = torch.from_numpy(np.ascontiguousarray(m.indptr, dtype=np.int32)).to(dev)
+        indices = torch.from_numpy(np.ascontiguousarray(m.indices, dtype=np.int32)).to(dev)
+        data = torch.from_numpy(np.ascontiguousarray(m.data, dtype=np.float32)).to(dev)
+        return cls(indptr, indices, data, m.shape, symmetric=symmetric, validate=validate)
+
+    def validate(self):
+        """Device-side CSR check (monotone indptr, indices in range) -- one sync."""
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        with torch.cuda.device(self.device):
+            call("gcg_csr_validate", self.n_rows, self.n_cols, self.nnz, _ptr(self.indptr),
+                 _ptr(self.indices), _ptr(status), _stream_handle(self.device))
+        code = int(status.item())
+        if code != 0:
+            raise ValueError(f"invalid CSR (gcg_status {code}): indptr must be monotone from 0 "
+                             "to nnz and every column index in [0, n_cols)")
+
+    def to_scipy(self) -> sps.csr_matrix:
+        return sps.csr_matrix((self.data.cpu().numpy(), self.indices.cpu().numpy(),
+                               self.indptr.cpu().numpy()), shape=self.shape)
+
+    # -- plans & transpose --------------------------------------------------------------
+    def plan(self, rows: Optional[RowSelection] = None, ordered: bool = False,
+             task_nnz: int = 0) -> Plan:
+        key = (rows.key if rows is not None else None, bool(ordered), int(task_nnz))
+        p = self._plans.get(key)
+        if p is None:
+            p = Plan(self, rows, ordered, task_nnz)
+            self._plans[key] = p
+        return p
+
+    def transpose(self) -> "DeviceCSR":
+        """CSR of A^T built on the device (stable: within a row, entries keep A's order).
+        For a symmetric operator (H, by construction) this is A itself."""
+        if self.symmetric:
+            return self
+        if self._transpose is None:
+            out_indptr = torch.empty(self.n_cols + 1, dtype=torch.int32, device=self.device)
+            out_indices = torch.empty(self.nnz, dtype=torch.int32, device=self.device)
+            out_vals = torch.empty(self.nnz, dtype=torch.float32, device=self.device)
+            need = C.c_size_t()
+            stream = _stream_handle(self.device)
+            with torch.cuda.device(self.device):
+                call("gcg_csr_transpose_f32", self.n_rows, self.n_cols, self.nnz, None, None, None,
+                     None, None, None, None, 0, C.byref(need), stream)
+                ws = torch.empty(max(need.value, 1), dtype=torch.uint8, device=self.device)
+                call("gcg_csr_transpose_f32", self.n_rows, self.n_cols, self.nnz,
+                     _ptr(self.indptr), _ptr(self.indices), _ptr(self.data), _ptr(out_indptr),
+                     _ptr(out_indices), _ptr(out_vals), _ptr(ws), need.value, None, stream)
+            t = DeviceCSR(out_indptr, out_indices, out_vals, (self.n_cols, self.n_rows),
+                          validate=False)
+            t._transpose = self
+            self._transpose = t
+        return self._transpose
+
+    def __repr__(self):
+        return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
+
+
+def _check_dense(Z: torch.Tensor, A: DeviceCSR):
+    _require_cuda(Z, "Z")
+    if Z.dtype != torch.float32:
+        raise TypeError(f"Z must be float32, got {Z.dtype}")
+    if Z.dim() != 2 or Z.shape[0] != A.n_cols:
+        raise ValueError(f"shape mismatch: A is {A.shape}, Z is {tuple(Z.shape)}")
+    if Z.stride(1) != 1 and Z.shape[1] > 1:
+        Z = Z.contiguous()
+    return Z
+
+
+def empty_dense(n: int, k: int, device, pad_to: int = 4) -> torch.Tensor:
+    """[n, k] float32 view of an [n, round_up(k, pad_to)] buffer: rows 16-B aligned, so
+    the kernels can use dwordx4 loads/stores whatever K is."""
+    ld = (k + pad_to - 1) // pad_to * pad_to if k > 0 else 0
+    buf = torch.empty((n, ld), dtype=torch.float32, device=device)
+    return buf[:, :k] if ld != k else buf
+
+
+def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         act: Optional[str] = None, rows=None, mode: str = "fast",
+         out: Optional[torch.Tensor] = None, task_nnz: int = 0) -> torch.Tensor:
+    """Y = act(A . Z + bias)[rows] on the GPU (S.dot of mlpconv.py:71,73,90 + epilogue).
+
+    mode  'fast'    : planned; rows longer than task_nnz split across waves (|err| <= 1e-5)
+          'ordered' : planned, rows never split -> bitwise scipy float32
+          'rowwise' : plan-less, one wave per output row -> bitwise scipy float32
+    rows : None | RowSelection | int array -- output row subset (target_indices).
+           A plain array/tensor runs plan-less (no plan to cache).
+    """
+    if not isinstance(A, DeviceCSR):
+        raise ValueError("Input for this layer must be sparse")
+    if mode not in MODES:
+        raise ValueError(f"mode must be one of {MODES}")
+    if act not in ACTS:
+        raise ValueError(f"unsupported activation {act!r}")
+    Z = _check_dense(Z, A)
+    K = Z.shape[1]
+    sel = None
+    rows_dev = None
+    if rows is not None:
+        if isinstance(rows, RowSelection):
+            sel = rows
+        elif isinstance(rows, torch.Tensor) and rows.is_cuda:
+            rows_dev = rows.to(torch.int32).contiguous()
+            mode = "rowwise"
+            if rows_dev.numel() and (int(rows_dev.min()) < 0 or int(rows_dev.max()) >= A.n_rows):
+                raise IndexError("rows out of range")
+        else:
+            sel = RowSelection(rows, device=A.device)
+        if sel is not None:
+            if sel.n and (int(sel.host.min()) < 0 or int(sel.host.max()) >= A.n_rows):
+                raise IndexError("rows out of range")
+            rows_dev = sel.device_rows
+    n_out = A.n_rows if rows_dev is None else int(rows_dev.numel())
+    if bias is not None:
+        _require_cuda(bias, "bias")
+        if bias.dtype != torch.float32 or bias.numel() != K:
+            raise ValueError(f"bias must be float32[{K}]")
+        bias = bias.contiguous()
+    if out is None:
+        out = empty_dense(n_out, K, A.device)
+    else:
+        _require_cuda(out, "out")
+        if out.shape != (n_out, K) or out.dtype != torch.float32 or (K > 1 and out.stride(1) != 1):
+            raise ValueError(f"out must be float32 [{n_out}, {K}] with unit column stride")
+    if n_out == 0 or K == 0:
+        return out
+    ldz = Z.stride(0) if Z.shape[0] > 1 else max(K, 1)
+    ldy = out.stride(0) if n_out > 1 else max(K, 1)
+    stream = _stream_handle(A.device)
+    actc = ACTS[act]
+    with torch.cuda.device(A.device):
+        if mode == "rowwise":
+            call("gcg_spmm_csr_f32", A.n_rows, A.n_cols, A.nnz, _ptr(A.indptr), _ptr(A.indices),
+                 _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(rows_dev),
+                 n_out, stream)
+        else:
+            plan = A.plan(sel, ordered=(mode == "ordered"), task_nnz=task_nnz)
+            ws = plan.workspace(K)
+            call("gcg_spmm_csr_f32_planned", plan.handle, _ptr(A.indptr), _ptr(A.indices),
+                 _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(ws),
+                 0 if ws is None else ws.numel() * 4, stream)
+    return out
+
+
+def index_csr(idx: torch.Tensor, n_rows: int):
+    """(seg_ptr, sorted_pos): CSR of an index list, stable (gcg_index_csr)."""
+    _require_cuda(idx, "idx")
+    idx = idx.to(torch.int32).contiguous()
+    n = idx.numel()
+    dev = idx.device
+    seg_ptr = torch.empty(n_rows + 1, dtype=torch.int32, device=dev)
+    sorted_pos = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    need = C.c_size_t()
+    stream = _stream_handle(dev)
+    with torch.cuda.device(dev):
+        call("gcg_index_csr", n, None, n_rows, None, None, None, 0, C.byref(need), stream)
+        ws = torch.empty(max(need.value, 1), dtype=torch.uint8, device=dev)
+        call("gcg_index_csr", n, _ptr(idx), n_rows, _ptr(seg_ptr), _ptr(sorted_pos), _ptr(ws),
+             need.value, None, stream)
+    return seg_ptr, sorted_pos
+
+
+def scatter_add_rows(out: torch.Tensor, seg_ptr: torch.Tensor, sorted_pos: torch.Tensor,
+                     src: torch.Tensor) -> torch.Tensor:
+    """out[idx[i]] += src[i] for all i, duplicates added in increasing i (gcg_scatter_add_rows_f32)."""
+    _require_cuda(out, "out")
+    _require_cuda(src, "src")
+    if src.stride(1) != 1 and src.shape[1] > 1:
+        src = src.contiguous()
+    n_rows, K = out.shape
+    if src.shape[1] != K:
+        raise ValueError("width mismatch")
+    lds = src.stride(0) if src.shape[0] > 1 else K
+    with torch.cuda.device(out.device):
+        call("gcg_scatter_add_rows_f32", n_rows, _ptr(seg_ptr), _ptr(sorted_pos), _ptr(src), lds, K,
+             _ptr(out), out.stride(0) if n_rows > 1 else K, _stream_handle(out.device))
+    return out

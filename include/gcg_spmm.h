@@ -1,0 +1,162 @@
+/*
+ * gcg_spmm.h -- C-ABI of the MI355X (gfx950) graph-convolution hot path.
+ *
+ * This is the drop-in boundary for the one hot path of afcarl/graphconvgeo:
+ * the normalized-adjacency x dense-features product Y = act(H . Z + b) that the
+ * reference computes with `theano.sparse.dot` (S.dot) inside its two Lasagne
+ * graph-convolution layers. Every entry point names the reference site it replaces.
+ *
+ *   reference                                   replaced by
+ *   ------------------------------------------  -----------------------------------
+ *   mlpconv.py:73   S.dot(self.H, activation)   gcg_spmm_csr_f32 / _planned
+ *   mlpconv.py:90   S.dot(self.H, activation)   (same; width C instead of K)
+ *   mlpconv.py:71   S.dot(input, self.W)        (same kernel: X (CSR N x F) . W1)
+ *   mlpconv.py:75-77 + b, rectify               fused epilogue: bias != NULL, act = GCG_ACT_RELU
+ *   mlpconv.py:92-94 + b, [target_indices, :]   fused epilogue: bias, out_rows subset
+ *   Theano grad of S.dot (x.T . gz)             gcg_spmm_* on CSR(H^T) (= H, H symmetric)
+ *                                               and CSR(X^T) from gcg_csr_transpose_f32
+ *   Theano grad of Y[target_indices] (inc_subtensor, duplicates add)
+ *                                               gcg_scatter_add_rows_f32
+ *
+ * Conventions (scipy CSR layout, as `scipy.sparse.csr_matrix` holds it):
+ *   indptr  int32[n_rows + 1], indices int32[nnz], vals float32[nnz]; dense operands
+ *   are row-major float32 with an explicit leading dimension (elements, >= K).
+ *   All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless the
+ *   parameter name ends in `_host`. Nothing in the hot path allocates, synchronizes,
+ *   or throws; every function returns a gcg_status (0 = ok). `stream` is a
+ *   hipStream_t (NULL = the legacy default stream). Calls are reentrant per stream;
+ *   the only global state is the per-thread last-error message.
+ *
+ * Numerics: per output element the products H[r,j]*Z[j,c] are accumulated in
+ * CSR storage order, each product and each sum rounded separately (no FMA).
+ * That is exactly scipy's `csr_matvecs` (the executor behind the reference's
+ * S.dot), so the plan-less and ordered paths match scipy float32 bit for bit.
+ * The planned fast path splits rows longer than its task size across waves and
+ * adds the per-segment partials in order: equal to scipy within 1e-5 (abs, on
+ * normalized-H inputs), not bitwise, for those rows only.
+ */
+#ifndef GCG_SPMM_H
+#define GCG_SPMM_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* gcg_stream_t; /* hipStream_t */
+
+typedef enum {
+  GCG_OK = 0,
+  GCG_ERR_INVALID_ARG = 1,  /* null pointer, negative or inconsistent size   */
+  GCG_ERR_MISALIGNED = 2,   /* pointer not 4-byte aligned                     */
+  GCG_ERR_HIP = 3,          /* a HIP runtime call or kernel launch failed     */
+  GCG_ERR_ALLOC = 4,        /* host or device allocation failed (plan create) */
+  GCG_ERR_BAD_CSR = 5,      /* indptr not monotone / out of range, bad index  */
+  GCG_ERR_WORKSPACE = 6     /* workspace missing or too small                 */
+} gcg_status;
+
+enum { GCG_ACT_NONE = 0, GCG_ACT_RELU = 1 };
+
+/* Library version, "major.minor.patch". */
+const char* gcg_version(void);
+/* Text of the last error raised on this host thread ("" if none). */
+const char* gcg_last_error(void);
+
+/*
+ * Plan-less SpMM, one 64-lane wave per output row, storage-order accumulation:
+ *   for i in [0, n_out):  r = out_rows ? out_rows[i] : i
+ *       Y[i, 0:K] = act( sum_{j in row r, storage order} vals[j] * Z[indices[j], 0:K] + bias )
+ * n_out == n_rows when out_rows == NULL. Bitwise equal to scipy float32 `H @ Z`
+ * (rows re-indexed by out_rows). Replaces S.dot at mlpconv.py:71,73,90 and the
+ * row gather at mlpconv.py:94. The CSR must be valid (see gcg_csr_validate).
+ */
+gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                            const int32_t* indptr, const int32_t* indices,
+                            const float* vals, const float* Z, int64_t ldz, int64_t K,
+                            float* Y, int64_t ldy, const float* bias, int act,
+                            const int32_t* out_rows, int64_t n_out,
+                            gcg_stream_t stream);
+
+/*
+ * nnz-balanced launch plan for one CSR (and one optional output-row list).
+ * Built once per H (H is shared by both layers and every epoch, mlpconv.py:214,293),
+ * reused for every K. Reads indptr (and out_rows) back to the host once and
+ * validates indptr; this call synchronizes `stream` -- it is NOT a hot-path call.
+ *   task_nnz  : target nonzeros per wave task (0 = default 512).
+ *   ordered   : 1 = never split a row (bitwise scipy order, long rows serial);
+ *               0 = split rows longer than task_nnz into segments (fast).
+ */
+typedef struct gcg_spmm_plan gcg_spmm_plan;
+
+gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_cols,
+                                int64_t nnz, const int32_t* indptr,
+                                const int32_t* out_rows, int64_t n_out, int64_t task_nnz,
+                                int ordered, gcg_stream_t stream);
+gcg_status gcg_spmm_plan_destroy(gcg_spmm_plan* plan);
+/* Bytes of device workspace gcg_spmm_csr_f32_planned needs for width K (0 if none). */
+gcg_status gcg_spmm_plan_workspace_bytes(const gcg_spmm_plan* plan, int64_t K, size_t* bytes);
+/* Plan statistics: wave tasks, rows split into segments, segments, max task nnz. */
+gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64_t* n_long_rows,
+                              int64_t* n_segments, int64_t* max_task_nnz);
+
+/* Planned SpMM: same contract as gcg_spmm_csr_f32; out_rows/n_out come from the plan. */
+gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                    const int32_t* indices, const float* vals,
+                                    const float* Z, int64_t ldz, int64_t K, float* Y,
+                                    int64_t ldy, const float* bias, int act, void* workspace,
+                                    size_t workspace_bytes, gcg_stream_t stream);
+
+/*
+ * Host-only planner (no device memory, no HIP calls): the task list the plan uses,
+ * exposed for testing and for host-side tools. `tasks_host` receives n_tasks int32
+ * quadruples {a, b, c, d}: d < 0 -> rows of positions [a, b); d >= 0 -> segment of
+ * position a covering nonzeros [b, c) into workspace slot d. `long_host` receives
+ * n_long quadruples {position, first_slot, n_slots, 0}. Pass NULL buffers to size.
+ */
+gcg_status gcg_spmm_plan_host(int64_t n_rows, const int32_t* indptr_host,
+                              const int32_t* out_rows_host, int64_t n_out, int64_t task_nnz,
+                              int ordered, int32_t* tasks_host, int64_t tasks_cap,
+                              int64_t* n_tasks, int32_t* long_host, int64_t long_cap,
+                              int64_t* n_long, int64_t* n_slots);
+
+/*
+ * Device CSR check: indptr[0] == 0, monotone, indptr[n_rows] == nnz, every
+ * index in [0, n_cols). Writes 0 (ok) or a gcg_status code to *status_dev
+ * (a device int32). Asynchronous on `stream`.
+ */
+gcg_status gcg_csr_validate(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                            const int32_t* indptr, const int32_t* indices,
+                            int32_t* status_dev, gcg_stream_t stream);
+
+/*
+ * Scatter-add of rows (backward of Y[target_indices] at mlpconv.py:94, where
+ * target indices repeat because train indices are drawn with replacement,
+ * tensormain.py:226):  for i in [0, n_idx): out[idx[i], 0:K] += src[i, 0:K].
+ * Deterministic: duplicates are added in increasing i, via the CSR of idx built
+ * by gcg_index_csr (sorted_pos/seg_ptr). `out` is NOT zeroed first.
+ */
+gcg_status gcg_index_csr(int64_t n_idx, const int32_t* idx, int64_t n_rows, int32_t* seg_ptr,
+                         int32_t* sorted_pos, void* workspace, size_t workspace_bytes,
+                         size_t* workspace_needed, gcg_stream_t stream);
+gcg_status gcg_scatter_add_rows_f32(int64_t n_rows, const int32_t* seg_ptr,
+                                    const int32_t* sorted_pos, const float* src, int64_t lds,
+                                    int64_t K, float* out, int64_t ldo, gcg_stream_t stream);
+
+/*
+ * CSR transpose on the device (CSR(X^T) for the X^T . dZ1 gradient of
+ * mlpconv.py:71). Output is sorted by (row, col) with stable order for equal
+ * entries. out_indptr int32[n_cols+1], out_indices int32[nnz], out_vals f32[nnz].
+ */
+gcg_status gcg_csr_transpose_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                 const int32_t* indptr, const int32_t* indices,
+                                 const float* vals, int32_t* out_indptr, int32_t* out_indices,
+                                 float* out_vals, void* workspace, size_t workspace_bytes,
+                                 size_t* workspace_needed, gcg_stream_t stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GCG_SPMM_H */

@@ -1,0 +1,125 @@
+"""CPU tests of the C-ABI library: it loads, exports every symbol include/gcg_spmm.h
+declares, and its host-only planner balances work (no GPU compute here)."""
+import ctypes as C
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "gcg_spmm.h")
+
+
+def declared_functions():
+    text = open(HEADER).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(gcg_[a-z0-9_]+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    names = declared_functions()
+    for must in ("gcg_spmm_csr_f32", "gcg_spmm_csr_f32_planned", "gcg_spmm_plan_create",
+                 "gcg_spmm_plan_destroy", "gcg_scatter_add_rows_f32", "gcg_csr_transpose_f32"):
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(native_lib):
+    from graphconvgeo_amd import _native
+    for name in declared_functions():
+        assert hasattr(native_lib, name), name
+        assert name in _native.SIGNATURES, f"{name} has no ctypes signature"
+    nm = subprocess.run(["nm", "-D", "--defined-only", _native.lib_path()], capture_output=True,
+                        text=True, check=True).stdout
+    exported = set(re.findall(r"\bT (gcg_[a-z0-9_]+)$", nm, flags=re.M))
+    assert set(declared_functions()) <= exported
+    assert _native.version() == "0.1.0"
+
+
+def test_header_compiles_as_c():
+    src = f'#include "{HEADER}"\nint main(void) {{ return GCG_OK; }}\n'
+    res = subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-x", "c", "-", "-o", "/dev/null"],
+                         input=src, capture_output=True, text=True)
+    assert res.returncode == 0, res.stderr
+
+
+def plan_host(indptr, task_nnz=512, ordered=0, rows=None):
+    from graphconvgeo_amd import _native
+    indptr = np.ascontiguousarray(indptr, dtype=np.int32)
+    rows_a = None if rows is None else np.ascontiguousarray(rows, dtype=np.int32)
+    n = indptr.size - 1
+    nt, nl, ns = C.c_int64(), C.c_int64(), C.c_int64()
+    args = (n, indptr.ctypes.data, None if rows_a is None else rows_a.ctypes.data,
+            0 if rows_a is None else rows_a.size, task_nnz, ordered)
+    _native.call("gcg_spmm_plan_host", *args, None, 0, C.byref(nt), None, 0, C.byref(nl), C.byref(ns))
+    tasks = np.zeros((max(nt.value, 1), 4), np.int32)
+    longs = np.zeros((max(nl.value, 1), 4), np.int32)
+    _native.call("gcg_spmm_plan_host", *args, tasks.ctypes.data, nt.value, C.byref(nt),
+                 longs.ctypes.data, nl.value, C.byref(nl), C.byref(ns))
+    return tasks[: nt.value], longs[: nl.value], ns.value
+
+
+@pytest.mark.parametrize("ordered", [0, 1])
+def test_planner_covers_every_row_once(native_lib, ordered):
+    rng = np.random.default_rng(0)
+    lens = rng.zipf(1.8, size=5000).clip(0, 20000)
+    lens[rng.random(5000) < 0.1] = 0
+    indptr = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+    tasks, longs, nslots = plan_host(indptr, task_nnz=256, ordered=ordered)
+    covered = np.zeros(5000, np.int64)
+    seg_nnz = np.zeros(5000, np.int64)
+    for a, b, c, d in tasks:
+        if d < 0:
+            covered[a:b] += 1
+            nnz = indptr[b] - indptr[a]
+            assert nnz <= 256 or b - a == 1  # a task over budget is a single (unsplit) row
+        else:
+            seg_nnz[a] += c - b
+            assert indptr[a] <= b < c <= indptr[a + 1] and 0 <= d < nslots
+            assert c - b <= 256
+    for p, first, cnt, _ in longs:
+        covered[p] += 1
+        assert seg_nnz[p] == lens[p]
+    assert np.all(covered == 1)
+    if ordered:
+        assert len(longs) == 0 and nslots == 0
+    else:
+        assert len(longs) == int((lens > 256).sum())
+
+
+def test_planner_row_subset_and_errors(native_lib):
+    from graphconvgeo_amd import _native
+    indptr = np.array([0, 2, 2, 700, 705], np.int32)
+    tasks, longs, ns = plan_host(indptr, task_nnz=100, rows=[3, 1, 1, 0])
+    assert all(t[3] < 0 for t in tasks) and len(longs) == 0
+    tasks, longs, ns = plan_host(indptr, task_nnz=100, rows=[2, 1, 1])
+    assert longs[:, 0].tolist() == [0] and ns == 7
+    with pytest.raises(_native.NativeError, match="INVALID_ARG"):
+        plan_host(indptr, rows=[9])
+    with pytest.raises(_native.NativeError, match="BAD_CSR"):
+        plan_host(np.array([0, 5, 3], np.int32))
+
+
+def test_row_partition_balance():
+    from graphconvgeo_amd.distributed import remap_columns, row_partition
+    rng = np.random.default_rng(1)
+    lens = rng.zipf(2.0, 10000).clip(1, 3000)
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    for P in (1, 2, 3, 8):
+        b = row_partition(indptr, P)
+        assert b[0] == 0 and b[-1] == 10000 and np.all(np.diff(b) >= 0)
+        cost = np.diff(indptr[b] + 2 * b)
+        assert cost.max() <= cost.sum() / P + lens.max() + 2
+    b = np.array([0, 3, 7, 10])
+    assert remap_columns(np.array([0, 2, 3, 6, 7, 9]), b, 4).tolist() == [0, 2, 4, 7, 8, 10]
+
+
+def test_product_path_refuses_cpu_tensors(native_lib):
+    import scipy.sparse as sps
+    import torch
+    from graphconvgeo_amd import sparse as gs
+    with pytest.raises(ValueError, match="CUDA"):
+        gs.DeviceCSR.from_scipy(sps.eye(3, format="csr", dtype=np.float32), "cpu")
+    with pytest.raises(ValueError, match="must be sparse"):
+        gs.DeviceCSR.from_scipy(np.eye(3), "cpu")

@@ -1,0 +1,91 @@
+"""GPU parity of the drop-in layers (mlpconv.py:59-95) and their backward pass."""
+import os
+
+import numpy as np
+import pytest
+import scipy.sparse as sps
+import torch
+
+from graphconvgeo_amd import sparse as gs
+from graphconvgeo_amd.layers import (GCN, ConvolutionDenseLayer, GraphConvLayer,
+                                     SparseConvolutionDenseLayer)
+from graphconvgeo_amd.synth import glorot_uniform, synthetic_features, synthetic_graph
+from oracle import gcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module")
+def g():
+    return dict(np.load(os.path.join(GOLD, "mention_graph.npz")))
+
+
+def golden_inputs(g):
+    n = int(g["n"])
+    H = sps.csr_matrix((g["H32_data"], g["H_indices"], g["H_indptr"]), shape=(n, n))
+    X = sps.csr_matrix((g["X_data"], g["X_indices"], g["X_indptr"]), shape=tuple(g["X_shape"]))
+    return H, X
+
+
+def test_layers_vs_golden(cuda, g):
+    H, X = golden_inputs(g)
+    F, K = g["W1"].shape
+    C = g["W2"].shape[1]
+    l1 = SparseConvolutionDenseLayer(F, H=H, num_units=K, W=g["W1"], b=g["b1"], device=cuda,
+                                     mode="ordered")
+    l2 = ConvolutionDenseLayer(l1, H=l1.H, num_units=C, W=g["W2"], b=g["b2"], device=cuda,
+                               mode="ordered")
+    assert l2.H is l1.H  # one device copy of H shared, as mlpconv.py:214
+    h = l1.get_output_for(X)
+    assert np.array_equal(h.detach().cpu().numpy(), g["h32"])  # bitwise scipy fp32
+    P = l2.get_output_for(h, target_indices=g["idx"])
+    assert np.abs(P.detach().cpu().numpy() - g["P64"]).max() < 1e-5
+    loss = -torch.log(P[torch.arange(P.shape[0]), torch.from_numpy(g["y"]).long().to(cuda)]).mean()
+    loss.backward()
+    for p, ref in ((l1.W, g["gW1_64"]), (l2.W, g["gW2_64"]), (l1.b, g["gb1_64"]), (l2.b, g["gb2_64"])):
+        got = p.grad.cpu().numpy()
+        assert np.abs(got - ref).max() < 1e-5 * max(1.0, np.abs(ref).max())
+
+
+def test_sparse_input_required(cuda, g):
+    H, X = golden_inputs(g)
+    l1 = SparseConvolutionDenseLayer(X.shape[1], H=H, num_units=4, device=cuda)
+    with pytest.raises(ValueError, match="must be sparse"):
+        l1(torch.zeros(X.shape, device=cuda))
+
+
+@pytest.mark.parametrize("mode", ["fast", "ordered"])
+def test_gcn_medium_fwd_bwd(cuda, mode):
+    n, f, k, c = 30_000, 2_000, 300, 129
+    H = synthetic_graph(n, 250_000)
+    X = synthetic_features(n, f, nnz_per_row=32, empty_frac=0.02)
+    W1, W2 = glorot_uniform(f, k), glorot_uniform(k, c, seed=9)
+    b1 = np.random.default_rng(1).standard_normal(k).astype(np.float32) * 0.01
+    b2 = np.zeros(c, np.float32)
+    idx = np.random.default_rng(2).choice(20_000, size=20_000).astype(np.int32)  # with replacement
+    y = np.random.default_rng(3).integers(0, c, size=idx.size)
+    model = GCN(H, X, f, k, c, device=cuda, W1=W1, W2=W2, mode=mode)
+    with torch.no_grad():
+        model.l_hid1.b.copy_(torch.from_numpy(b1))
+    P = model(idx)
+    loss = torch.nn.functional.nll_loss(torch.log(P), torch.from_numpy(y).to(cuda))
+    loss.backward()
+    fwd = O.gcn_forward(X, H, W1, b1, W2, b2, idx)
+    assert np.abs(P.detach().cpu().numpy() - fwd["P"]).max() < 1e-5
+    gr = O.gcn_backward(X, H, W1, W2, fwd, idx, y, regul_coefs=(0.0, 0.0))
+    for p, key in ((model.l_hid1.W, "W1"), (model.l_out.W, "W2"), (model.l_hid1.b, "b1"),
+                   (model.l_out.b, "b2")):
+        ref = gr[key]
+        assert np.abs(p.grad.cpu().numpy() - ref).max() < 1e-5 * max(1.0, np.abs(ref).max()), key
+
+
+def test_graphconvlayer_dense_input_and_nonlinearities(cuda):
+    H = synthetic_graph(3_000, 20_000)
+    h = np.random.default_rng(0).standard_normal((3_000, 40)).astype(np.float32)
+    W = glorot_uniform(40, 30)
+    lay = GraphConvLayer(40, H=H, num_units=30, W=W, b=0.5, nonlinearity="tanh", device=cuda,
+                         mode="ordered")
+    out = lay(torch.from_numpy(h).to(cuda)).detach().cpu().numpy()
+    ref = np.tanh(O.spmm_f64(H, h.astype(np.float64) @ W.astype(np.float64)) + 0.5)
+    assert np.abs(out - ref).max() < 1e-5

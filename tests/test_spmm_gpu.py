@@ -1,0 +1,210 @@
+"""GPU parity of the HIP SpMM (S.dot, mlpconv.py:71,73,90) against the CPU oracle.
+
+Bar: 'rowwise' and 'ordered' modes are bitwise equal to the oracle (= scipy float32
+csr_matvecs); 'fast' mode is within 1e-5 absolute of the float64 product on
+normalized-H inputs (BASELINE.json north_star tolerance) and bitwise on every row it
+does not split.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sps
+import torch
+
+from graphconvgeo_amd import sparse as gs
+from graphconvgeo_amd.synth import synthetic_graph, dense
+from oracle import gcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+TOL = 1e-5  # north_star: "outputs match the Theano/scipy CPU reference within 1e-5 fp32"
+
+
+def rand_csr(n_rows, n_cols, density_rows, seed, long_rows=(), empty_frac=0.1, sort=True,
+             dups=False):
+    rng = np.random.default_rng(seed)
+    lens = rng.poisson(density_rows, size=n_rows)
+    lens[rng.random(n_rows) < empty_frac] = 0
+    for r, L in long_rows:
+        lens[r] = L
+    indptr = np.zeros(n_rows + 1, dtype=np.int64)
+    np.cumsum(lens, out=indptr[1:])
+    nnz = int(indptr[-1])
+    indices = rng.integers(0, n_cols, size=nnz).astype(np.int32)
+    if not dups:
+        m = sps.csr_matrix((np.ones(nnz), indices, indptr), shape=(n_rows, n_cols))
+        m.sum_duplicates()
+        indptr, indices = m.indptr, m.indices.astype(np.int32)
+        nnz = indices.size
+    data = (rng.random(nnz) * 0.2 - 0.05).astype(np.float32)
+    m = sps.csr_matrix((data, indices, indptr.astype(np.int32)), shape=(n_rows, n_cols))
+    if not sort:
+        for i in range(n_rows):
+            s, e = m.indptr[i], m.indptr[i + 1]
+            p = rng.permutation(e - s) + s
+            m.indices[s:e] = m.indices[p]
+            m.data[s:e] = m.data[p]
+        m.has_sorted_indices = False
+    return m
+
+
+def to_dev(x, dev):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(dev)
+
+
+@pytest.mark.parametrize("K", [1, 3, 4, 8, 63, 64, 65, 129, 256, 300, 512, 513, 930, 1500])
+@pytest.mark.parametrize("mode", ["rowwise", "ordered"])
+def test_bitwise_vs_oracle(cuda, K, mode):
+    H = rand_csr(700, 500, 12, seed=K, long_rows=[(5, 3000), (600, 1500)])
+    Z = np.random.default_rng(K).standard_normal((500, K)).astype(np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    Y = gs.spmm(A, to_dev(Z, cuda), mode=mode).cpu().numpy()
+    ref = O.spmm_f32(H, Z)
+    assert np.array_equal(Y, ref), np.abs(Y - ref).max()
+
+
+@pytest.mark.parametrize("K", [1, 4, 65, 300, 930])
+@pytest.mark.parametrize("task_nnz", [16, 64, 512])
+def test_fast_mode_tolerance(cuda, K, task_nnz):
+    H = rand_csr(900, 800, 20, seed=7 + K, long_rows=[(3, 5000), (4, 700), (899, 2049)])
+    Z = np.random.default_rng(K).standard_normal((800, K)).astype(np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    Y = gs.spmm(A, to_dev(Z, cuda), mode="fast", task_nnz=task_nnz).cpu().numpy()
+    ref32 = O.spmm_f32(H, Z)
+    ref64 = O.spmm_f64(H, Z)
+    assert np.abs(Y - ref64).max() <= TOL + np.abs(ref32 - ref64).max()
+    lens = np.diff(H.indptr)
+    unsplit = lens <= task_nnz
+    assert np.array_equal(Y[unsplit], ref32[unsplit])
+    info = A.plan(None, False, task_nnz).info()
+    assert info["n_long_rows"] == int((~unsplit).sum())
+
+
+def test_normalized_graph_fast_within_1e5(cuda):
+    H = synthetic_graph(20_000, 200_000)  # power-law, hubs split in fast mode
+    Z = dense(20_000, 300)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    Y = gs.spmm(A, to_dev(Z, cuda), task_nnz=128).cpu().numpy()
+    ref64 = O.spmm_f64(H, Z)
+    assert np.abs(Y - ref64).max() <= TOL
+    assert A.plan(None, False, 128).info()["n_long_rows"] > 0
+
+
+@pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
+def test_bias_relu_and_rows_subset(cuda, mode):
+    H = rand_csr(400, 300, 9, seed=3, long_rows=[(17, 900)])
+    K = 129
+    Z = np.random.default_rng(1).standard_normal((300, K)).astype(np.float32)
+    b = np.random.default_rng(2).standard_normal(K).astype(np.float32)
+    rows = np.random.default_rng(4).integers(0, 400, size=250).astype(np.int32)
+    rows[:5] = 17  # duplicates, the long row (train indices are drawn with replacement)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    sel = gs.RowSelection(rows, cuda)
+    Y = gs.spmm(A, to_dev(Z, cuda), bias=to_dev(b, cuda), act="relu", rows=sel, mode=mode,
+                task_nnz=256).cpu().numpy()
+    ref = O.spmm_f32(H, Z, bias=b, act="relu", rows=rows)
+    if mode == "fast":
+        assert np.abs(Y - ref).max() <= 1e-5
+    else:
+        assert np.array_equal(Y, ref)
+    # plain cuda index tensor -> plan-less path
+    Y2 = gs.spmm(A, to_dev(Z, cuda), bias=to_dev(b, cuda), act="relu",
+                 rows=to_dev(rows, cuda)).cpu().numpy()
+    assert np.array_equal(Y2, ref)
+
+
+def test_unsorted_and_duplicate_entries(cuda):
+    H = rand_csr(300, 300, 15, seed=9, sort=False, dups=True)
+    assert not H.has_canonical_format
+    Z = np.random.default_rng(5).standard_normal((300, 64)).astype(np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    for mode in ("rowwise", "ordered"):
+        Y = gs.spmm(A, to_dev(Z, cuda), mode=mode).cpu().numpy()
+        assert np.array_equal(Y, O.spmm_f32(H, Z))
+        assert np.array_equal(Y, (H @ Z).astype(np.float32))  # scipy itself
+
+
+def test_strided_operands(cuda):
+    H = rand_csr(256, 200, 10, seed=11)
+    Zbig = np.random.default_rng(6).standard_normal((200, 310)).astype(np.float32)
+    Zt = to_dev(Zbig, cuda)[:, 5:305]  # ldz = 310, misaligned start -> scalar path
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    Y = gs.spmm(A, Zt).cpu().numpy()
+    assert np.array_equal(Y, O.spmm_f32(H, Zbig[:, 5:305]))
+    out = torch.full((256, 400), 7.0, device=cuda)
+    gs.spmm(A, Zt, out=out[:, :300])
+    assert torch.all(out[:, 300:] == 7.0)
+    assert np.array_equal(out[:, :300].cpu().numpy(), O.spmm_f32(H, Zbig[:, 5:305]))
+
+
+def test_edge_cases(cuda):
+    # all rows empty (nnz = 0): output = act(bias)
+    H = sps.csr_matrix((50, 40), dtype=np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    b = torch.linspace(-1, 1, 12, device=cuda)
+    Y = gs.spmm(A, torch.randn(40, 12, device=cuda), bias=b, act="relu")
+    assert torch.equal(Y, torch.relu(b).expand(50, 12))
+    # zero rows / zero width
+    H0 = sps.csr_matrix((0, 10), dtype=np.float32)
+    A0 = gs.DeviceCSR.from_scipy(H0, cuda)
+    assert gs.spmm(A0, torch.randn(10, 5, device=cuda)).shape == (0, 5)
+    A1 = gs.DeviceCSR.from_scipy(rand_csr(20, 10, 3, seed=1), cuda)
+    assert gs.spmm(A1, torch.randn(10, 0, device=cuda)).shape == (20, 0)
+    # one single huge row
+    Hh = rand_csr(3, 5000, 0, seed=2, long_rows=[(1, 4000)], empty_frac=0)
+    Z = np.random.default_rng(3).standard_normal((5000, 300)).astype(np.float32)
+    Ah = gs.DeviceCSR.from_scipy(Hh, cuda)
+    for mode in ("rowwise", "ordered"):
+        assert np.array_equal(gs.spmm(Ah, to_dev(Z, cuda), mode=mode).cpu().numpy(), O.spmm_f32(Hh, Z))
+    Yf = gs.spmm(Ah, to_dev(Z, cuda), mode="fast").cpu().numpy()
+    assert np.abs(Yf - O.spmm_f64(Hh, Z)).max() < 1e-4
+
+
+def test_errors(cuda):
+    H = rand_csr(20, 10, 3, seed=1)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    with pytest.raises(ValueError):
+        gs.spmm(A, torch.randn(11, 4, device=cuda))
+    with pytest.raises(TypeError):
+        gs.spmm(A, torch.randn(10, 4, device=cuda, dtype=torch.float64))
+    with pytest.raises(ValueError):
+        gs.spmm(A, torch.randn(10, 4))  # CPU tensor: no fallback
+    with pytest.raises(ValueError, match="must be sparse"):
+        gs.spmm(np.zeros((3, 3)), torch.randn(3, 4, device=cuda))
+    bad = sps.csr_matrix((np.ones(3, np.float32), np.array([0, 1, 99], np.int32),
+                          np.array([0, 2, 3], np.int32)), shape=(2, 10), copy=False)
+    with pytest.raises(ValueError, match="invalid CSR"):
+        gs.DeviceCSR.from_scipy(bad, cuda)
+
+
+def test_transpose_and_scatter_add(cuda):
+    X = rand_csr(500, 120, 8, seed=21, long_rows=[(3, 100)])
+    A = gs.DeviceCSR.from_scipy(X, cuda)
+    T = A.transpose().to_scipy()
+    ref = X.T.tocsr()  # scipy csr transpose: stable within a row
+    assert np.array_equal(T.indptr, ref.indptr)
+    assert np.array_equal(T.indices, ref.indices)
+    assert np.array_equal(T.data, ref.data)
+    # X^T . G (the dW1 gradient, mlpconv.py:71) bitwise = scipy on the transposed CSR
+    G = np.random.default_rng(2).standard_normal((500, 300)).astype(np.float32)
+    Y = gs.spmm(A.transpose(), to_dev(G, cuda), mode="ordered").cpu().numpy()
+    assert np.array_equal(Y, O.spmm_f32(ref, G))
+    # scatter-add with duplicate indices
+    idx = np.random.default_rng(3).integers(0, 50, size=400).astype(np.int32)
+    src = np.random.default_rng(4).standard_normal((400, 33)).astype(np.float32)
+    base = np.random.default_rng(5).standard_normal((50, 33)).astype(np.float32)
+    seg_ptr, pos = gs.index_csr(to_dev(idx, cuda), 50)
+    out = to_dev(base.copy(), cuda)
+    gs.scatter_add_rows(out, seg_ptr, pos, to_dev(src, cuda))
+    assert np.array_equal(out.cpu().numpy(), O.scatter_add_f32(base.copy(), idx, src))
+
+
+def test_geotext_scale_vs_oracle(cuda):
+    """Config 2: GEOTEXT-scale graph, hidden 300, fp32 parity vs the CPU reference."""
+    H = synthetic_graph(9_475, 80_000)
+    Z = dense(9_475, 300)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    Zd = to_dev(Z, cuda)
+    ref = O.spmm_f32(H, Z)
+    assert np.array_equal(gs.spmm(A, Zd, mode="ordered").cpu().numpy(), ref)
+    assert np.array_equal(gs.spmm(A, Zd, mode="rowwise").cpu().numpy(), ref)
+    assert np.abs(gs.spmm(A, Zd, mode="fast").cpu().numpy() - O.spmm_f64(H, Z)).max() <= TOL
