@@ -94,6 +94,12 @@ def load_traffic(workload: str, per_launch_bytes: int):
         return None, None
 
 
+def resolve_mode(A, mode: str) -> str:
+    if mode != "auto":
+        return mode
+    return "ordered" if A.max_row_nnz() * gs.AUTO_SPLIT_RATIO <= max(A.nnz, 1) else "fast"
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -102,10 +108,13 @@ def main():
     ap.add_argument("--config", default="twitter-world", choices=sorted(CONFIGS))
     ap.add_argument("--graph", default="powerlaw", choices=["powerlaw", "uniform"])
     ap.add_argument("--hidden", type=int, default=None, help="K (default: config hidden=300)")
-    ap.add_argument("--mode", default="fast", choices=list(gs.MODES))
+    ap.add_argument("--mode", default="auto", choices=list(gs.MODES))
     ap.add_argument("--task-nnz", type=int, default=0)
+    ap.add_argument("--ld", type=int, default=0, help="row stride of Z/Y in floats (0 = K rounded to 4)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--partitioned", action="store_true",
+                    help="use the row-partitioned (all-gather) path even at N = 1")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -129,12 +138,14 @@ def main():
 
     gen = torch.Generator(device=dev)
     gen.manual_seed(SEED + rank)
-    if world == 1:
+    if world == 1 and not args.partitioned:
         A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
-        Z = torch.randn((N, K), generator=gen, device=dev, dtype=torch.float32)
-        Y = gs.empty_dense(N, K, dev)
+        ld = max(args.ld, K)
+        Z = torch.randn((N, ld), generator=gen, device=dev, dtype=torch.float32)[:, :K]
+        Y = gs.empty_dense(N, K, dev) if args.ld == 0 else torch.empty((N, ld), device=dev)[:, :K]
         gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)  # builds the plan
-        info = A.plan(None, args.mode == "ordered", args.task_nnz).info() if args.mode != "rowwise" else {}
+        eff = resolve_mode(A, args.mode)
+        info = A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
 
         def step():
             gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)
@@ -145,7 +156,8 @@ def main():
         Zl = torch.randn((part.block_rows, K), generator=gen, device=dev, dtype=torch.float32)
         Y = gs.empty_dense(part.n_local, K, dev)
         part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
-        info = part.A.plan(None, args.mode == "ordered", args.task_nnz).info() if args.mode != "rowwise" else {}
+        eff = resolve_mode(part.A, args.mode)
+        info = part.A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
 
         def step():
             part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
@@ -173,7 +185,7 @@ def main():
 
     # Live per-launch kernel time with HIP events on the SpMM's own stream (N = 1 roofline).
     roofline = None
-    if world == 1 and args.steps > 0:
+    if world == 1 and not args.partitioned and args.steps > 0:
         stream = torch.cuda.current_stream(dev)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
@@ -184,7 +196,7 @@ def main():
         torch.cuda.synchronize(dev)
         k_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
         achieved = B / (k_ms * 1e-3) / 1e9
-        workload = f"{args.config}-{args.graph}-k{K}-{args.mode}"
+        workload = f"{args.config}-{args.graph}-k{K}-{eff}"
         traffic, traffic_src = load_traffic(workload, B)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
@@ -201,7 +213,7 @@ def main():
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "edges_per_s": round(nnz / (ms * 1e-3), 1),
         "config": {"workload": f"{cfg.name} H.Z SpMM fwd, {args.graph} degrees", "nodes": N,
-                   "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": args.mode,
+                   "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": f"{args.mode}->{eff}",
                    "parallelism": f"row{world}" if world > 1 else "single",
                    "plan": info, "graph_gen_s": round(t_gen, 1)},
     }

@@ -33,6 +33,7 @@
 #include <cstring>
 #include <new>
 #include <string>
+#include <utility>
 #include <vector>
 
 #include "../../include/gcg_spmm.h"
@@ -362,9 +363,16 @@ struct HostPlan {
   int64_t max_task_nnz = 0;
 };
 
+// Default task size: 512 nonzeros, smaller on small graphs so the launch still has
+// >= ~8k waves (256 CUs x 32 waves) to spread; never below 32.
+int64_t default_task_nnz(int64_t nnz) {
+  int64_t w = nnz / 8192;
+  return w < 32 ? 32 : (w > kDefaultTaskNnz ? kDefaultTaskNnz : w);
+}
+
 gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t* out_rows,
                            int64_t n_out, int64_t task_nnz, int ordered, HostPlan* hp) {
-  if (task_nnz <= 0) task_nnz = kDefaultTaskNnz;
+  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows]);
   if (indptr[0] != 0) return fail(GCG_ERR_BAD_CSR, "indptr[0] = %d != 0", indptr[0]);
   for (int64_t r = 0; r < n_rows; ++r)
     if (indptr[r + 1] < indptr[r]) return fail(GCG_ERR_BAD_CSR, "indptr decreases at row %lld", (long long)r);
@@ -373,6 +381,7 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   hp->n_slots = 0;
   hp->max_task_nnz = 0;
   std::vector<int32_t> seg_tasks;
+  std::vector<std::pair<int64_t, int64_t>> long_rows;  // (nnz, position), ordered mode
   int64_t cur_begin = -1, cur_cost = 0, cur_nnz = 0;
   auto close = [&](int64_t end) {
     if (cur_begin >= 0) {
@@ -400,6 +409,13 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
       hp->n_slots += nseg;
       continue;
     }
+    if (ordered && len > task_nnz) {
+      // Unsplittable long row (bitwise mode): its own task, scheduled first (LPT) so the
+      // serial tail of a hub row overlaps the bulk instead of ending the launch.
+      close(p);
+      long_rows.push_back({len, p});
+      continue;
+    }
     const int64_t cost = len + kRowCost;
     if (cur_begin >= 0 && cur_cost + cost > task_nnz) close(p);
     if (cur_begin < 0) cur_begin = p;
@@ -407,8 +423,20 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
     cur_nnz += len;
   }
   close(n_out);
-  // Segments first: they are the longest-running tasks of split rows.
-  hp->tasks.insert(hp->tasks.begin(), seg_tasks.begin(), seg_tasks.end());
+  // Longest work first: unsplit long rows (ordered mode) by descending length, then the
+  // segments of split rows, then the short-row tasks in row order.
+  std::stable_sort(long_rows.begin(), long_rows.end(),
+                   [](const std::pair<int64_t, int64_t>& a, const std::pair<int64_t, int64_t>& b) {
+                     return a.first > b.first;
+                   });
+  std::vector<int32_t> head;
+  head.reserve(long_rows.size() * 4 + seg_tasks.size());
+  for (const auto& lr : long_rows) {
+    head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -1, -1});
+    hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
+  }
+  head.insert(head.end(), seg_tasks.begin(), seg_tasks.end());
+  hp->tasks.insert(hp->tasks.begin(), head.begin(), head.end());
   if (hp->tasks.size() / 4 > static_cast<size_t>(INT32_MAX)) return fail(GCG_ERR_INVALID_ARG, "too many tasks");
   return GCG_OK;
 }
@@ -513,7 +541,7 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
   gcg_spmm_plan* p = new (std::nothrow) gcg_spmm_plan();
   if (p == nullptr) return fail(GCG_ERR_ALLOC, "plan allocation failed");
   p->n_rows = n_rows; p->n_cols = n_cols; p->nnz = nnz; p->n_out = n_out;
-  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : kDefaultTaskNnz;
+  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz);
   p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
   p->n_long = static_cast<int>(hp.longs.size() / 4);
   p->n_slots = hp.n_slots;

@@ -103,7 +103,7 @@ def _index_csr_cached(rows: gs.RowSelection, n_rows: int):
 
 def csr_matmul(A: gs.DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
                act: Optional[str] = None, rows: Optional[gs.RowSelection] = None,
-               mode: str = "fast") -> torch.Tensor:
+               mode: str = "auto") -> torch.Tensor:
     """Differentiable S.dot(A, Z) (+ bias, rectify, row subset) through the HIP kernels."""
     return _CSRMatMul.apply(Z, bias, A, act, rows, mode)
 
@@ -136,7 +136,7 @@ class GraphConvLayer(nn.Module):
 
     def __init__(self, incoming=None, H=None, num_units: int = None, W=None, b=0.0,
                  nonlinearity="rectify", device: Union[str, torch.device] = "cuda",
-                 mode: str = "fast", require_sparse_input: bool = False, generator=None,
+                 mode: str = "auto", require_sparse_input: bool = False, generator=None,
                  in_features: Optional[int] = None):
         super().__init__()
         if num_units is None:
@@ -217,7 +217,7 @@ class GCN(nn.Module):
     """
 
     def __init__(self, H, X, in_features: int, hidden: int, n_classes: int,
-                 device="cuda", W1=None, W2=None, mode: str = "fast", generator=None):
+                 device="cuda", W1=None, W2=None, mode: str = "auto", generator=None):
         super().__init__()
         self.device = torch.device(device)
         Hd = _as_device_csr(H, self.device)

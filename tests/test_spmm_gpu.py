@@ -208,3 +208,24 @@ def test_geotext_scale_vs_oracle(cuda):
     assert np.array_equal(gs.spmm(A, Zd, mode="ordered").cpu().numpy(), ref)
     assert np.array_equal(gs.spmm(A, Zd, mode="rowwise").cpu().numpy(), ref)
     assert np.abs(gs.spmm(A, Zd, mode="fast").cpu().numpy() - O.spmm_f64(H, Z)).max() <= TOL
+
+
+def test_row_partitioned_device_path_world1(cuda):
+    """RowPartitionedCSR on the GPU (world = 1): gather buffer, column remap, HIP SpMM."""
+    from graphconvgeo_amd.distributed import RowPartitionedCSR
+    H = synthetic_graph(5_000, 40_000)
+    Z = dense(5_000, 300)
+    part = RowPartitionedCSR(H, 0, 1, cuda)
+    Y = part.spmm(to_dev(Z, cuda), mode="ordered").cpu().numpy()
+    assert np.array_equal(Y, O.spmm_f32(H, Z))
+    # explicit 3-way bounds, each "rank" computed in turn on the one device (no collective)
+    bounds = np.array([0, 1700, 3300, 5000])
+    got = np.zeros_like(Y)
+    for r in range(3):
+        p = RowPartitionedCSR(H, r, 3, cuda, bounds=bounds)
+        full = torch.zeros((3 * p.block_rows, 300), device=cuda)
+        for q in range(3):
+            full[q * p.block_rows: q * p.block_rows + bounds[q + 1] - bounds[q]] = \
+                to_dev(Z[bounds[q]:bounds[q + 1]], cuda)
+        got[bounds[r]:bounds[r + 1]] = gs.spmm(p.A, full, mode="ordered").cpu().numpy()
+    assert np.array_equal(got, O.spmm_f32(H, Z))

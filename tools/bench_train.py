@@ -1,0 +1,91 @@
+#!/usr/bin/env python
+"""BASELINE config 3: Twitter-US-scale 2-layer GCN fwd+bwd (+ Adam) step on one MI355X.
+
+One step = MLPCONV's full-batch epoch (mlpconv.py:293-295): X.W1, H.Z1 (+b1, rectify),
+h.W2, (H.Z2 + b2)[train], CE + L1/L2, backward (scatter-add, H.g, h^T.g, g.W2^T, H.g,
+X^T.g) and the Lasagne Adam update. Synthetic data (seed 77): power-law graph, 64-nnz/row
+BoW X, 60 % of nodes as train indices drawn with replacement (tensormain.py:226).
+Prints one JSON line (ms/step, per-SpMM algorithmic bytes summed -> effective GB/s).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+from graphconvgeo_amd import sparse as gs  # noqa: E402
+from graphconvgeo_amd.mlpconv import LasagneAdam, MLPCONV  # noqa: E402
+from graphconvgeo_amd.synth import CONFIGS, synthetic_features, synthetic_graph  # noqa: E402
+
+
+def spmm_bytes(n_rows, nnz, K):
+    return 4 * (n_rows + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n_rows
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="twitter-us", choices=sorted(CONFIGS))
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nnz-per-row", type=int, default=64)
+    ap.add_argument("--mode", default="auto")
+    args = ap.parse_args()
+    cfg = CONFIGS[args.config]
+    dev = torch.device("cuda:0")
+    t0 = time.perf_counter()
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges)
+    X = synthetic_features(cfg.n_nodes, cfg.n_features, nnz_per_row=args.nnz_per_row)
+    t_gen = time.perf_counter() - t0
+    n = cfg.n_nodes
+    rng = np.random.default_rng(77)
+    Y = rng.integers(0, cfg.n_classes, size=n)
+    Y[:cfg.n_classes] = np.arange(cfg.n_classes)
+    n_tr = int(0.6 * n)
+    train = rng.choice(n_tr, size=n_tr).astype(np.int32)
+    dev_idx = np.arange(n_tr, int(0.8 * n), dtype=np.int32)
+    test_idx = np.arange(int(0.8 * n), n, dtype=np.int32)
+
+    clf = MLPCONV(n_epochs=0, hidden_layer_size=cfg.hidden, device=dev, seed=1, mode=args.mode)
+    clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H/X, no epochs
+    y_train = torch.as_tensor(Y[train].astype(np.int64), device=dev)
+    opt = LasagneAdam(clf.params)
+
+    def step():
+        opt.zero_grad()
+        loss, _acc = clf._loss_acc(clf.rows["train"], y_train)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) / args.steps * 1e3
+    K, C = cfg.hidden, cfg.n_classes
+    nnzH, nnzX = H.nnz, X.nnz
+    # SpMMs per step: X.W1, H.Z1, H.Z2 (train rows only), H.g2, H.g1, X^T.g
+    sp = (spmm_bytes(n, nnzX, K) + spmm_bytes(n, nnzH, K) + spmm_bytes(n, nnzH, C) +
+          spmm_bytes(n, nnzH, K) + spmm_bytes(cfg.n_features, nnzX, K))
+    sp_fwd_rows = spmm_bytes(len(train), int(np.diff(H.indptr)[train].sum()), C)
+    total = sp + sp_fwd_rows
+    rec = {"metric": "GCN 2-layer fwd+bwd+adam step", "config": cfg.name, "ms_per_step": round(ms, 3),
+           "nodes": n, "nnz_H": nnzH, "nnz_X": nnzX, "F": cfg.n_features, "K": K, "C": C,
+           "train_rows": len(train), "spmm_algorithmic_bytes_per_step": total,
+           "spmm_effective_GBps_if_all_time_in_spmm": round(total / (ms * 1e-3) / 1e9, 1),
+           "mode": args.mode, "data_gen_s": round(t_gen, 1)}
+    print(json.dumps(rec), flush=True)
+
+
+if __name__ == "__main__":
+    main()
