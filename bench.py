@@ -113,6 +113,8 @@ def main():
     ap.add_argument("--ld", type=int, default=0, help="row stride of Z/Y in floats (0 = K rounded to 4)")
     ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--chunks", type=int, default=2,
+                    help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned (all-gather) path even at N = 1")
     args = ap.parse_args()
@@ -151,16 +153,15 @@ def main():
             gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)
     else:
         from graphconvgeo_amd.distributed import RowPartitionedCSR
-        import torch.distributed as dist
         part = RowPartitionedCSR(H, rank, world, dev)
         Zl = torch.randn((part.block_rows, K), generator=gen, device=dev, dtype=torch.float32)
         Y = gs.empty_dense(part.n_local, K, dev)
-        part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
         eff = resolve_mode(part.A, args.mode)
+        part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
         info = part.A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
 
         def step():
-            part.spmm(Zl, out=Y, mode=args.mode, task_nnz=args.task_nnz)
+            part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
 
     def barrier():
         if world > 1:
@@ -205,6 +206,33 @@ def main():
         if traffic_src:
             roofline["traffic_source"] = traffic_src
 
+    # N > 1 (or --partitioned): the two phases alone, max over ranks, for the comm fraction.
+    dist_info = None
+    if world > 1 or args.partitioned:
+        def timed(fn, reps):
+            barrier()
+            t0 = time.perf_counter()
+            for _ in range(reps):
+                fn()
+            barrier()
+            dt = (time.perf_counter() - t0) / reps * 1e3
+            if world > 1:
+                import torch.distributed as dist
+                tt = torch.tensor([dt], dtype=torch.float64, device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                dt = float(tt.item())
+            return dt
+        reps = max(args.steps // 2, 1)
+        full = part.all_gather(Zl)
+        t_comm = timed(lambda: part.all_gather(Zl), reps)
+        t_sp = timed(lambda: gs.spmm(part.A, full, out=Y, mode=eff, task_nnz=args.task_nnz), reps)
+        gathered = (world - 1) * part.block_rows * K * 4
+        dist_info = {"allgather_ms": round(t_comm, 4), "local_spmm_ms": round(t_sp, 4),
+                     "allgather_inbound_GBps_per_gpu": round(gathered / (t_comm * 1e-3) / 1e9, 1),
+                     "chunks": args.chunks, "rows_local": part.n_local,
+                     "nnz_local": part.nnz_local, "block_rows": part.block_rows,
+                     "spmm_only_aggregate_GBps": round(B / (t_sp * 1e-3) / 1e9, 1)}
+
     value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
@@ -219,6 +247,8 @@ def main():
     }
     if roofline:
         rec["roofline"] = roofline
+    if dist_info:
+        rec["distributed"] = dist_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(H, K, args.cpu_budget)
     if rank == 0:

@@ -30,6 +30,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <new>
 #include <string>
@@ -310,10 +311,21 @@ int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K
 }
 
 // Returns panel width (floats) and launches.
+int panel_override() {
+  static const int v = [] {
+    const char* e = std::getenv("GCG_PANEL");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
 gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
   const int64_t K = a.K;
+  const int req = panel_override();  // experiment knob: panel width in floats
+  if (req > 0)
+    while (vec > 1 && kWave * vec > req) vec /= 2;
   const int per_chunk = kWave * vec;
-  const int nch_max = kPanelMax / per_chunk;
+  const int nch_max = req > 0 ? std::max(1, std::min(kPanelMax, req) / per_chunk) : kPanelMax / per_chunk;
   int nch = static_cast<int>((K + per_chunk - 1) / per_chunk);
   if (nch > nch_max) nch = nch_max;
   if (nch < 1) nch = 1;

@@ -101,3 +101,53 @@ class RowPartitionedCSR:
     def spmm(self, Z_local: torch.Tensor, **kw) -> torch.Tensor:
         """Y_local = (H . Z)[start:stop] = H_p . all_gather(Z)."""
         return self._spmm(self.A, self.all_gather(Z_local), **kw)
+
+    # -- pipelined: all-gather of column chunk c+1 overlaps the SpMM of chunk c -----------
+    @staticmethod
+    def chunk_bounds(K: int, n_chunks: int):
+        """Column chunks of ~K/n_chunks, every boundary a multiple of 4 floats (16-B rows)."""
+        n_chunks = max(1, min(n_chunks, (K + 3) // 4))
+        step = ((K + n_chunks - 1) // n_chunks + 3) // 4 * 4
+        b = list(range(0, K, step)) + [K]
+        return [(b[i], b[i + 1]) for i in range(len(b) - 1)]
+
+    def _pipe_buffers(self, K: int, n_chunks: int):
+        key = ("pipe", K, n_chunks)
+        bufs = self._gather_buf.get(key)
+        if bufs is None:
+            bufs = []
+            for c0, c1 in self.chunk_bounds(K, n_chunks):
+                w = c1 - c0
+                send = torch.zeros((self.block_rows, w), dtype=torch.float32, device=self.device)
+                recv = torch.zeros((self.world * self.block_rows, w), dtype=torch.float32,
+                                   device=self.device)
+                bufs.append((c0, c1, send, recv))
+            self._gather_buf[key] = bufs
+        return bufs
+
+    def spmm_pipelined(self, Z_local: torch.Tensor, out: torch.Tensor, n_chunks: int = 4,
+                       **kw) -> torch.Tensor:
+        """Same result as spmm() (bitwise: each output column is computed by the same
+        kernel in the same storage order); comm of chunk c+1 hides behind compute of c."""
+        K = Z_local.shape[1]
+        bufs = self._pipe_buffers(K, n_chunks)
+        rows = Z_local.shape[0]
+        for c0, c1, send, _recv in bufs:
+            send[:rows].copy_(Z_local[:, c0:c1])
+        works = [None] * len(bufs)
+
+        def start(i):
+            _c0, _c1, send, recv = bufs[i]
+            if self.world == 1:
+                recv.copy_(send)
+            else:
+                works[i] = dist.all_gather_into_tensor(recv, send, group=self.group, async_op=True)
+
+        start(0)
+        for i, (c0, c1, _send, recv) in enumerate(bufs):
+            if i + 1 < len(bufs):
+                start(i + 1)
+            if works[i] is not None:
+                works[i].wait()  # the compute stream waits for this chunk only
+            self._spmm(self.A, recv, out=out[:, c0:c1], **kw)
+        return out

@@ -23,9 +23,13 @@ def _free_port():
     return p
 
 
-def _oracle_spmm(A, Z_full, **kw):
+def _oracle_spmm(A, Z_full, out=None, **kw):
     from oracle import gcn_oracle as O
-    return torch.from_numpy(O.spmm_f32(A, Z_full.numpy()))
+    Y = torch.from_numpy(O.spmm_f32(A, Z_full.numpy()))
+    if out is not None:
+        out.copy_(Y)
+        return out
+    return Y
 
 
 def _worker(rank, world, port, n, e, K, q):
@@ -38,6 +42,9 @@ def _worker(rank, world, port, n, e, K, q):
         part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm)
         Zl = torch.from_numpy(part.local_rows(Z).copy())
         Y = part.spmm(Zl)
+        Yp = torch.empty_like(Y)
+        part.spmm_pipelined(Zl, Yp, n_chunks=3)  # 24 cols -> chunks of 8
+        assert torch.equal(Y, Yp)
         out = [None] * world
         dist.all_gather_object(out, (part.start, part.stop, Y.numpy()))
         if rank == 0:

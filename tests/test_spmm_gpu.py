@@ -229,3 +229,14 @@ def test_row_partitioned_device_path_world1(cuda):
                 to_dev(Z[bounds[q]:bounds[q + 1]], cuda)
         got[bounds[r]:bounds[r + 1]] = gs.spmm(p.A, full, mode="ordered").cpu().numpy()
     assert np.array_equal(got, O.spmm_f32(H, Z))
+
+
+@pytest.mark.parametrize("chunks", [1, 3, 4])
+def test_pipelined_partition_bitwise(cuda, chunks):
+    from graphconvgeo_amd.distributed import RowPartitionedCSR
+    H = synthetic_graph(4_000, 30_000)
+    Z = dense(4_000, 300)
+    part = RowPartitionedCSR(H, 0, 1, cuda)
+    Y = gs.empty_dense(4_000, 300, cuda)
+    part.spmm_pipelined(to_dev(Z, cuda), Y, n_chunks=chunks, mode="ordered")
+    assert np.array_equal(Y.cpu().numpy(), O.spmm_f32(H, Z))

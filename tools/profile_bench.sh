@@ -2,6 +2,8 @@
 # Profile one bench.py workload on the GPU box: kernel-trace stats + separate PMC passes
 # (FETCH_SIZE, WRITE_SIZE, TCC hit/miss), summarised into gpurun_out/prof_<tag>_<workload>/pmc_<workload>.json.
 # usage: tools/profile_bench.sh <round-tag> <bench args...>   (run from the repo root)
+# The workload name uses the effective mode: bench's default 'auto' resolves to 'ordered'
+# on the World graphs, so pass --mode explicitly when profiling anything else.
 set -o pipefail
 tag=$1; shift
 export TMPDIR=/tmp
@@ -9,7 +11,7 @@ cfg=$(python3 - "$@" <<'PY'
 import sys, argparse
 ap = argparse.ArgumentParser(); ap.add_argument("--config", default="twitter-world")
 ap.add_argument("--graph", default="powerlaw"); ap.add_argument("--hidden", type=int, default=300)
-ap.add_argument("--mode", default="fast"); a, _ = ap.parse_known_args(sys.argv[1:])
+ap.add_argument("--mode", default="ordered"); a, _ = ap.parse_known_args(sys.argv[1:])
 print(f"{a.config}-{a.graph}-k{a.hidden}-{a.mode}")
 PY
 )
