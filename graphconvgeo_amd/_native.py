@@ -46,6 +46,8 @@ SIGNATURES = {
     "gcg_scatter_add_rows_f32": (C.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p]),
     "gcg_csr_transpose_f32": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p,
                                         C.c_size_t, _psz, _p]),
+    "gcg_normalize_adjacency_f32": (C.c_int, [_i64, _i64, _p, _p, C.c_int, _p, _p, _p, _p, _p,
+                                              C.c_size_t, _psz, _p, _p]),
 }
 
 _lock = threading.Lock()

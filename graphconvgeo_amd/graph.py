@@ -77,3 +77,44 @@ def csr_from_edges(n: int, u: np.ndarray, v: np.ndarray, dtype=np.float32,
     data = (dinv[rows] * dinv[cols]).astype(dtype)
     idx_t = np.int32 if (n < 2**31 and len(cols) < 2**31) else np.int64
     return sps.csr_matrix((data, cols.astype(idx_t), indptr.astype(idx_t)), shape=(n, n))
+
+
+def normalize_edges_device(n: int, u, v, device="cuda", self_loops: bool = True):
+    """tensormain.py:170-180 on the GPU: undirected edges -> DeviceCSR H (canonical order,
+    duplicates collapsed), values bitwise equal to `csr_from_edges` / the reference's
+    float64 D*adj*D cast to float32 (gcg_normalize_adjacency_f32). One sync to read nnz."""
+    import ctypes as C
+
+    import torch
+
+    from . import sparse as gs
+    from ._native import call
+
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError("normalize_edges_device builds H in HBM: device must be a CUDA (HIP) device")
+    ut = torch.as_tensor(np.asarray(u), dtype=torch.int32).to(dev).contiguous()
+    vt = torch.as_tensor(np.asarray(v), dtype=torch.int32).to(dev).contiguous()
+    if ut.shape != vt.shape:
+        raise ValueError("u and v must have the same length")
+    e = int(ut.numel())
+    cap = 2 * e + (n if self_loops else 0)
+    indptr = torch.empty(n + 1, dtype=torch.int32, device=dev)
+    indices = torch.empty(max(cap, 1), dtype=torch.int32, device=dev)
+    vals = torch.empty(max(cap, 1), dtype=torch.float32, device=dev)
+    nnz = torch.zeros(1, dtype=torch.int64, device=dev)
+    status = torch.zeros(1, dtype=torch.int32, device=dev)
+    need = C.c_size_t()
+    stream = C.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+    with torch.cuda.device(dev):
+        call("gcg_normalize_adjacency_f32", n, e, None, None, int(self_loops), None, None, None,
+             None, None, 0, C.byref(need), None, stream)
+        ws = torch.empty(max(need.value, 1), dtype=torch.uint8, device=dev)
+        call("gcg_normalize_adjacency_f32", n, e, C.c_void_p(ut.data_ptr()), C.c_void_p(vt.data_ptr()),
+             int(self_loops), C.c_void_p(indptr.data_ptr()), C.c_void_p(indices.data_ptr()),
+             C.c_void_p(vals.data_ptr()), C.c_void_p(nnz.data_ptr()), C.c_void_p(ws.data_ptr()),
+             need.value, None, C.c_void_p(status.data_ptr()), stream)
+    if int(status.item()) != 0:
+        raise ValueError("edge endpoint out of range [0, n)")
+    m = int(nnz.item())
+    return gs.DeviceCSR(indptr, indices[:m], vals[:m], (n, n), symmetric=True, validate=False)

@@ -17,6 +17,7 @@
  *                                               and CSR(X^T) from gcg_csr_transpose_f32
  *   Theano grad of Y[target_indices] (inc_subtensor, duplicates add)
  *                                               gcg_scatter_add_rows_f32
+ *   tensormain.py:170-180 H = D^-1/2 (A+I) D^-1/2  gcg_normalize_adjacency_f32
  *
  * Conventions (scipy CSR layout, as `scipy.sparse.csr_matrix` holds it):
  *   indptr  int32[n_rows + 1], indices int32[nnz], vals float32[nnz]; dense operands
@@ -154,6 +155,23 @@ gcg_status gcg_csr_transpose_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
                                  const float* vals, int32_t* out_indptr, int32_t* out_indices,
                                  float* out_vals, void* workspace, size_t workspace_bytes,
                                  size_t* workspace_needed, gcg_stream_t stream);
+
+/*
+ * Graph operator on the device (tensormain.py:170-180): from an undirected edge list
+ * (u[e], v[e]) build H = D^-1/2 (A + I) D^-1/2 as a canonical CSR (rows and columns
+ * sorted; duplicate edges collapse to one binary entry, as networkx stores one edge per
+ * pair). H_ij = float32(float64(d_i^-1/2) * float64(d_j^-1/2)) with d = row degree incl.
+ * the self loop: bitwise the reference's float64 D*adj*D product after .astype(float32)
+ * (tensormain.py:221). Capacity: indices/vals hold 2*n_edges + n entries; the actual nnz
+ * is written to *nnz_dev (device int64). *status_dev = GCG_ERR_BAD_CSR on an endpoint out
+ * of [0, n). Pass all-NULL outputs to size the workspace.
+ */
+gcg_status gcg_normalize_adjacency_f32(int64_t n, int64_t n_edges, const int32_t* u,
+                                       const int32_t* v, int self_loops, int32_t* indptr,
+                                       int32_t* indices, float* vals, int64_t* nnz_dev,
+                                       void* workspace, size_t workspace_bytes,
+                                       size_t* workspace_needed, int32_t* status_dev,
+                                       gcg_stream_t stream);
 
 #ifdef __cplusplus
 }
