@@ -118,3 +118,16 @@ def normalize_edges_device(n: int, u, v, device="cuda", self_loops: bool = True)
         raise ValueError("edge endpoint out of range [0, n)")
     m = int(nnz.item())
     return gs.DeviceCSR(indptr, indices[:m], vals[:m], (n, n), symmetric=True, validate=False)
+
+
+def normalized_values_f64(H):
+    """float64 entries of H = D^-1/2 (A+I) D^-1/2 for a DeviceCSR built by
+    normalize_edges_device (d_i = row length): the operator main.py:522 multiplies X by
+    before any float32 cast."""
+    import torch
+
+    deg = (H.indptr[1:] - H.indptr[:-1]).to(torch.float64)
+    dinv = torch.where(deg > 0, 1.0 / torch.sqrt(deg), torch.zeros_like(deg))
+    rows = torch.repeat_interleave(torch.arange(H.n_rows, device=H.device),
+                                   (H.indptr[1:] - H.indptr[:-1]).long())
+    return dinv[rows] * dinv[H.indices.long()]

@@ -210,6 +210,50 @@ class ConvolutionDenseLayer(GraphConvLayer):
                          nonlinearity=nonlinearity, **kw)
 
 
+class SparseInputDenseLayer(nn.Module):
+    """lasagne_layers.py:20-29 (and mlpconv.py:27-36): nonlinearity(S.dot(X, W) + b), X sparse.
+
+    The input layer of the MDN heads (lang2loc.py:285); the same HIP SpMM (X . W gathers
+    rows of W) with bias + rectify fused. Lasagne's DenseLayer default nonlinearity is
+    rectify."""
+
+    def __init__(self, incoming=None, num_units: int = None, W=None, b=0.0,
+                 nonlinearity="rectify", device: Union[str, torch.device] = "cuda",
+                 mode: str = "auto", generator=None, in_features: Optional[int] = None):
+        super().__init__()
+        if num_units is None:
+            raise ValueError("num_units is required")
+        self.device = torch.device(device)
+        self.num_inputs = in_features if in_features is not None else _num_inputs(incoming)
+        self.num_units = int(num_units)
+        w = _glorot_uniform(self.num_inputs, self.num_units, generator) if W is None else W
+        self.W = nn.Parameter(_as_tensor(w, (self.num_inputs, self.num_units), self.device))
+        if b is None:
+            self.b = None
+        else:
+            bb = np.full(self.num_units, float(b), np.float32) if np.isscalar(b) else b
+            self.b = nn.Parameter(_as_tensor(bb, (self.num_units,), self.device))
+        self.fused_act, self.post = _resolve_nonlinearity(nonlinearity)
+        self.mode = mode
+        self._cache = {}
+
+    def forward(self, input, **kwargs):
+        if isinstance(input, gs.DeviceCSR):
+            X = input
+        elif sps.issparse(input):
+            key = (id(input), input.shape, input.nnz)
+            if key not in self._cache:
+                self._cache = {key: gs.DeviceCSR.from_scipy(input, self.device)}
+            X = self._cache[key]
+        else:
+            raise ValueError("Input for this layer must be sparse")
+        Y = csr_matmul(X, self.W, self.b, self.fused_act, None, self.mode)
+        return self.post(Y) if self.post is not None else Y
+
+    def get_output_for(self, input, **kwargs):
+        return self.forward(input, **kwargs)
+
+
 class GCN(nn.Module):
     """The 2-layer model MLPCONV.fit builds (mlpconv.py:196-217), inputs resident in HBM.
 

@@ -338,3 +338,39 @@ def scatter_add_rows(out: torch.Tensor, seg_ptr: torch.Tensor, sorted_pos: torch
         call("gcg_scatter_add_rows_f32", n_rows, _ptr(seg_ptr), _ptr(sorted_pos), _ptr(src), lds, K,
              _ptr(out), out.stride(0) if n_rows > 1 else K, _stream_handle(out.device))
     return out
+
+
+def spgemm(A: DeviceCSR, B: DeviceCSR, accumulate_f64: bool = False,
+           a_data64: Optional[torch.Tensor] = None) -> DeviceCSR:
+    """C = A . B on the GPU (the input convolution X_conv = H * X, main.py:530).
+
+    a_data64: float64 values of A (the reference's H is float64 there; implies float64
+    accumulation). Entries are summed in scipy's csr_matmat order; exact zeros dropped;
+    output canonical float32 (= `(H * X).tocsr().astype('float32')`)."""
+    if not isinstance(A, DeviceCSR) or not isinstance(B, DeviceCSR):
+        raise ValueError("spgemm operands must be DeviceCSR")
+    if A.n_cols != B.n_rows:
+        raise ValueError(f"shape mismatch {A.shape} x {B.shape}")
+    dev = A.device
+    stream = _stream_handle(dev)
+    P = C.c_int64()
+    with torch.cuda.device(dev):
+        call("gcg_spgemm_products", A.n_rows, A.nnz, _ptr(A.indptr), _ptr(A.indices), B.n_rows,
+             _ptr(B.indptr), C.byref(P), stream)
+        cap = max(P.value, 1)
+        c_ptr = torch.empty(A.n_rows + 1, dtype=torch.int32, device=dev)
+        c_idx = torch.empty(cap, dtype=torch.int32, device=dev)
+        c_val = torch.empty(cap, dtype=torch.float32, device=dev)
+        nnz = torch.zeros(1, dtype=torch.int64, device=dev)
+        if a_data64 is not None:
+            _require_cuda(a_data64, "a_data64")
+            if a_data64.dtype != torch.float64 or a_data64.numel() != A.nnz:
+                raise ValueError("a_data64 must be float64[nnz(A)]")
+            a_vals, is64, acc64 = a_data64.contiguous(), 1, 1
+        else:
+            a_vals, is64, acc64 = A.data, 0, int(bool(accumulate_f64))
+        call("gcg_spgemm", A.n_rows, A.n_cols, B.n_cols, A.nnz, _ptr(A.indptr), _ptr(A.indices),
+             _ptr(a_vals), is64, B.nnz, _ptr(B.indptr), _ptr(B.indices), _ptr(B.data), acc64,
+             P.value, _ptr(c_ptr), _ptr(c_idx), _ptr(c_val), _ptr(nnz), stream)
+    m = int(nnz.item())
+    return DeviceCSR(c_ptr, c_idx[:m], c_val[:m], (A.n_rows, B.n_cols), validate=False)

@@ -18,6 +18,7 @@
  *   Theano grad of Y[target_indices] (inc_subtensor, duplicates add)
  *                                               gcg_scatter_add_rows_f32
  *   tensormain.py:170-180 H = D^-1/2 (A+I) D^-1/2  gcg_normalize_adjacency_f32
+ *   main.py:530 / tensormain.py:114 X_conv = H * X gcg_spgemm_products + gcg_spgemm
  *
  * Conventions (scipy CSR layout, as `scipy.sparse.csr_matrix` holds it):
  *   indptr  int32[n_rows + 1], indices int32[nnz], vals float32[nnz]; dense operands
@@ -172,6 +173,27 @@ gcg_status gcg_normalize_adjacency_f32(int64_t n, int64_t n_edges, const int32_t
                                        void* workspace, size_t workspace_bytes,
                                        size_t* workspace_needed, int32_t* status_dev,
                                        gcg_stream_t stream);
+
+/*
+ * SpGEMM C = A . B for the host "input convolution" X_conv = H * X (main.py:530,
+ * tensormain.py:114; then .tocsr().astype('float32')). A: m x n CSR (values float32, or
+ * float64 when a_is_f64 -- the reference's H is float64 there), B: n x p CSR float32.
+ * Every C entry is summed in scipy csr_matmat's traversal order (A row order, then B row
+ * order), each product and sum rounded in the accumulation type (accumulate_f64 = 1:
+ * float64, the reference's H64 * X32 upcast), exact zero sums dropped (as scipy), then
+ * rounded to float32. Output CSR is canonical (sorted columns), as astype() leaves it.
+ * Step 1: gcg_spgemm_products -> number of products P (synchronizes). Step 2: gcg_spgemm
+ * with c_idx/c_val of capacity P, c_ptr of m+1; actual nnz to *nnz_c_dev. Not a hot-path
+ * call: it allocates stream-ordered temporaries (~32 B per product) and synchronizes.
+ */
+gcg_status gcg_spgemm_products(int64_t m, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
+                               int64_t n, const int32_t* b_ptr, int64_t* n_products,
+                               gcg_stream_t stream);
+gcg_status gcg_spgemm(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int32_t* a_ptr,
+                      const int32_t* a_idx, const void* a_val, int a_is_f64, int64_t nnz_b,
+                      const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
+                      int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
+                      float* c_val, int64_t* nnz_c_dev, gcg_stream_t stream);
 
 #ifdef __cplusplus
 }

@@ -89,3 +89,20 @@ def test_graphconvlayer_dense_input_and_nonlinearities(cuda):
     out = lay(torch.from_numpy(h).to(cuda)).detach().cpu().numpy()
     ref = np.tanh(O.spmm_f64(H, h.astype(np.float64) @ W.astype(np.float64)) + 0.5)
     assert np.abs(out - ref).max() < 1e-5
+
+
+def test_sparse_input_dense_layer(cuda):
+    from graphconvgeo_amd.layers import SparseInputDenseLayer
+    X = synthetic_features(5_000, 800, nnz_per_row=24, empty_frac=0.05)
+    W = glorot_uniform(800, 100)
+    b = np.random.default_rng(0).standard_normal(100).astype(np.float32) * 0.1
+    lay = SparseInputDenseLayer(800, num_units=100, W=W, b=b, device=cuda, mode="ordered")
+    out = lay(X)
+    ref = O.spmm_f32(X, W, bias=b, act="relu")
+    assert np.array_equal(out.detach().cpu().numpy(), ref)  # bitwise scipy fp32 + epilogue
+    out.sum().backward()
+    g = (ref > 0).astype(np.float64)
+    gW = sps.csr_matrix(X, dtype=np.float64).T @ g
+    assert np.abs(lay.W.grad.cpu().numpy() - gW).max() < 1e-4
+    with pytest.raises(ValueError, match="must be sparse"):
+        lay(torch.zeros((5, 800), device=cuda))
