@@ -115,6 +115,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
+                         "rehearse several ranks on one GPU)")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned (all-gather) path even at N = 1")
     args = ap.parse_args()
@@ -124,11 +127,15 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local_rank)
-    dev = torch.device("cuda", local_rank)
+    dev_index = local_rank % max(torch.cuda.device_count(), 1)
+    torch.cuda.set_device(dev_index)
+    dev = torch.device("cuda", dev_index)
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=dev)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cfg = CONFIGS[args.config]
     K = args.hidden or cfg.hidden
@@ -184,27 +191,39 @@ def main():
         elapsed = float(t.item())
     ms = elapsed / args.steps * 1e3
 
-    # Live per-launch kernel time with HIP events on the SpMM's own stream (N = 1 roofline).
+    # Live per-launch kernel time with HIP events on the SpMM's own stream. N = 1: the whole
+    # graph; N > 1: this rank's local SpMM on the gathered operand (local algorithmic bytes).
     roofline = None
-    if world == 1 and not args.partitioned and args.steps > 0:
+    if args.steps > 0:
+        if world == 1 and not args.partitioned:
+            kstep, kbytes = step, B
+        else:
+            full_k = part.all_gather(Zl)
+            kbytes = spmm_bytes(part.n_local, part.nnz_local, K)
+
+            def kstep():
+                gs.spmm(part.A, full_k, out=Y, mode=eff, task_nnz=args.task_nnz)
+            kstep()
         stream = torch.cuda.current_stream(dev)
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in range(args.steps)]
         for a, b in evs:
             a.record(stream)
-            step()
+            kstep()
             b.record(stream)
         torch.cuda.synchronize(dev)
         k_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
-        achieved = B / (k_ms * 1e-3) / 1e9
+        achieved = kbytes / (k_ms * 1e-3) / 1e9
         workload = f"{args.config}-{args.graph}-k{K}-{eff}"
-        traffic, traffic_src = load_traffic(workload, B)
+        traffic, traffic_src = load_traffic(workload, B) if kbytes == B else (None, None)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
-                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": B}
+                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": kbytes}
         if traffic_src:
             roofline["traffic_source"] = traffic_src
+        if kbytes != B:
+            roofline["scope"] = f"rank {rank} local SpMM ({part.n_local} rows, {part.nnz_local} nnz)"
 
     # N > 1 (or --partitioned): the two phases alone, max over ranks, for the comm fraction.
     dist_info = None
