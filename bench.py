@@ -9,8 +9,9 @@ the S.dot(H, .) of mlpconv.py:73. Inputs are resident in HBM before the timed re
   value     = algorithmic bytes per step / step time (GB/s), bytes per SURVEY.md §8d:
               B = 4(N+1) + 8 nnz + 4 K nnz + 4 K N
   edges/s   = nnz(H) / step time
-  N > 1     : H row-partitioned (nnz-balanced) over N ranks, each step = RCCL all-gather of
-              Z over xGMI + local SpMM; total work fixed -> "strong" scaling.
+  N > 1     : H row-partitioned (nnz-balanced) over N ranks, each step = RCCL exchange of Z
+              over xGMI (all-gather, or halo all-to-all of only the referenced rows) pipelined
+              with the local SpMM over column chunks; total work fixed -> "strong" scaling.
 
 Run: python bench.py [--gpus N --steps K --warmup W]; N > 1 under torch.distributed.run.
 """
@@ -115,6 +116,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "halo"],
+                    help="N > 1: all-gather every block, or send only the referenced halo rows")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -160,8 +163,8 @@ def main():
             gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)
     else:
         from graphconvgeo_amd.distributed import RowPartitionedCSR
-        part = RowPartitionedCSR(H, rank, world, dev)
-        Zl = torch.randn((part.block_rows, K), generator=gen, device=dev, dtype=torch.float32)
+        part = RowPartitionedCSR(H, rank, world, dev, exchange=args.exchange)
+        Zl = torch.randn((part.local_block_rows, K), generator=gen, device=dev, dtype=torch.float32)
         Y = gs.empty_dense(part.n_local, K, dev)
         eff = resolve_mode(part.A, args.mode)
         part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
@@ -245,9 +248,11 @@ def main():
         full = part.all_gather(Zl)
         t_comm = timed(lambda: part.all_gather(Zl), reps)
         t_sp = timed(lambda: gs.spmm(part.A, full, out=Y, mode=eff, task_nnz=args.task_nnz), reps)
-        gathered = (world - 1) * part.block_rows * K * 4
-        dist_info = {"allgather_ms": round(t_comm, 4), "local_spmm_ms": round(t_sp, 4),
-                     "allgather_inbound_GBps_per_gpu": round(gathered / (t_comm * 1e-3) / 1e9, 1),
+        gathered = part.exchange_bytes_per_row(K)
+        dist_info = {"exchange": part.exchange, "halo_fraction": round(part.halo_fraction, 4),
+                     "exchange_bytes_in_per_gpu": gathered,
+                     "exchange_ms": round(t_comm, 4), "local_spmm_ms": round(t_sp, 4),
+                     "exchange_inbound_GBps_per_gpu": round(gathered / (t_comm * 1e-3) / 1e9, 1),
                      "chunks": args.chunks, "rows_local": part.n_local,
                      "nnz_local": part.nnz_local, "block_rows": part.block_rows,
                      "spmm_only_aggregate_GBps": round(B / (t_sp * 1e-3) / 1e9, 1)}

@@ -32,14 +32,15 @@ def _oracle_spmm(A, Z_full, out=None, **kw):
     return Y
 
 
-def _worker(rank, world, port, n, e, K, q):
+def _worker(rank, world, port, n, e, K, q, exchange):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphconvgeo_amd.distributed import RowPartitionedCSR
         H = synthetic_graph(n, e)
         Z = np.random.default_rng(5).standard_normal((n, K)).astype(np.float32)
-        part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm)
+        part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm, exchange=exchange)
+        assert part.exchange == exchange
         Zl = torch.from_numpy(part.local_rows(Z).copy())
         Y = part.spmm(Zl)
         Yp = torch.empty_like(Y)
@@ -53,14 +54,15 @@ def _worker(rank, world, port, n, e, K, q):
         dist.destroy_process_group()
 
 
+@pytest.mark.parametrize("exchange", ["allgather", "halo"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_row_partitioned_spmm_equals_full(world):
+def test_row_partitioned_spmm_equals_full(world, exchange):
     from oracle import gcn_oracle as O
     n, e, K = 3000, 20000, 24
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, e, K, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n, e, K, q, exchange)) for r in range(world)]
     for p in procs:
         p.start()
     out = q.get(timeout=120)
@@ -78,3 +80,25 @@ def test_row_partitioned_spmm_equals_full(world):
     assert covered == n
     # Same per-row storage order -> bitwise equal to the unpartitioned product.
     assert np.array_equal(got, ref)
+
+
+def test_halo_layout_and_auto_choice():
+    from graphconvgeo_amd.distributed import RowPartitionedCSR
+    n, e = 3000, 20000
+    H = synthetic_graph(n, e)
+    Z = np.random.default_rng(1).standard_normal((n, 8)).astype(np.float32)
+    parts = [RowPartitionedCSR(H, r, 4, "cpu", local_spmm=_oracle_spmm, exchange="halo")
+             for r in range(4)]
+    for p in parts:
+        # own rows first, then the halo rows of rank 0..3 (sorted global ids)
+        b = p.bounds
+        assert sum(p.recv_counts) == p.halo_rows and p.recv_counts[p.rank] == 0
+        for q in parts:
+            assert q.send_counts[p.rank] == p.recv_counts[q.rank]
+        cols = np.unique(H.indices[H.indptr[b[p.rank]]:H.indptr[b[p.rank + 1]]])
+        halo = cols[(cols < p.start) | (cols >= p.stop)]
+        operand = np.concatenate([Z[p.start:p.stop], Z[halo]])
+        from oracle import gcn_oracle as O
+        assert np.array_equal(O.spmm_f32(p.local_host, operand), O.spmm_f32(H, Z)[p.start:p.stop])
+    dense = RowPartitionedCSR(H, 0, 2, "cpu", local_spmm=_oracle_spmm)  # halo ~100% -> allgather
+    assert dense.halo_fraction > 0.9 and dense.exchange == "allgather"

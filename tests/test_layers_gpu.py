@@ -103,6 +103,6 @@ def test_sparse_input_dense_layer(cuda):
     out.sum().backward()
     g = (ref > 0).astype(np.float64)
     gW = sps.csr_matrix(X, dtype=np.float64).T @ g
-    assert np.abs(lay.W.grad.cpu().numpy() - gW).max() < 1e-4
+    assert np.abs(lay.W.grad.cpu().numpy() - gW).max() < 1e-5 * np.abs(gW).max()  # fp32 sums of ~10^3 terms
     with pytest.raises(ValueError, match="must be sparse"):
         lay(torch.zeros((5, 800), device=cuda))
