@@ -64,7 +64,8 @@ class MLPCONV:
                  hidden_layer_size=None, drop_out=False, dropout_coefs=(0.5, 0.5),
                  early_stopping_max_down=100000, loss_name="log", nonlinearity="rectify",
                  dtype="float32", device="cuda", seed: Optional[int] = None, mode: str = "auto",
-                 model_file: Optional[str] = None, report_k_epoch: int = 10):
+                 model_file: Optional[str] = None, report_k_epoch: int = 10,
+                 order: str = "reference"):
         if dtype != "float32":
             raise ValueError("the GPU path computes in float32 (mlpconv.py dtype='float32')")
         if drop_out:
@@ -87,6 +88,7 @@ class MLPCONV:
         self.mode = mode
         self.model_file = model_file
         self.report_k_epoch = report_k_epoch
+        self.order = order  # ConvolutionDenseLayer order: reference | propagate_first | auto
         self.history = []
 
     # -- model --------------------------------------------------------------------------
@@ -105,7 +107,7 @@ class MLPCONV:
                                                   mode=self.mode, generator=gen)
         self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=out_size,
                                            W=W2, nonlinearity=None, device=self.device,
-                                           mode=self.mode, generator=gen)
+                                           mode=self.mode, generator=gen, order=self.order)
         if self.init_parameters is not None:
             with torch.no_grad():
                 self.l_hid1.b.copy_(torch.as_tensor(self.init_parameters[1]))

@@ -58,3 +58,18 @@ def test_mlpconv_api(cuda, tmp_path):
     assert (tmp_path / "best.pt").exists()
     with pytest.raises(ValueError):
         clf.predict("nope")
+
+
+def test_mlpconv_propagate_first_order(cuda):
+    """Reassociated layer 2 ((H.h)[idx].W2) tracks the reference-order oracle within tolerance."""
+    H, X, Y, train, dev, test, init = problem(c=60)  # C > K: auto picks propagate_first
+    coefs = (1e-5, 1e-5)
+    clf = MLPCONV(n_epochs=12, hidden_layer_size=48, regul_coefs=coefs, init_parameters=init,
+                  device=cuda, report_k_epoch=4, order="auto")
+    clf.fit(X, train, dev, test, Y, H)
+    assert clf.l_out.order == "propagate_first"
+    hist, _ = O.mlpconv_train(X, H, Y, train, dev, *init, n_epochs=12, regul_coefs=coefs,
+                              report_k_epoch=4)
+    got = np.array([h["train_loss"] for h in clf.history])
+    ref = np.array([h["train_loss"] for h in hist])
+    assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max()), (got, ref)
