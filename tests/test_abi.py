@@ -123,3 +123,22 @@ def test_product_path_refuses_cpu_tensors(native_lib):
         gs.DeviceCSR.from_scipy(sps.eye(3, format="csr", dtype=np.float32), "cpu")
     with pytest.raises(ValueError, match="must be sparse"):
         gs.DeviceCSR.from_scipy(np.eye(3), "cpu")
+
+
+def test_abi_argument_validation_without_gpu(native_lib):
+    """Entry points validate sizes/pointers before touching the device."""
+    from graphconvgeo_amd import _native
+    lib = native_lib
+    # negative sizes, NULL outputs, bad activation, ld < K
+    assert lib.gcg_spmm_csr_f32(-1, 1, 0, None, None, None, None, 1, 1, None, 1, None, 0, None, 0, None) == 1
+    assert lib.gcg_spmm_csr_f32(2, 2, 0, None, None, None, None, 4, 4, None, 4, None, 0, None, 0, None) == 1
+    assert lib.gcg_spmm_plan_create(None, 1, 1, 0, None, None, 0, 0, 0, None) == 1
+    assert lib.gcg_spmm_plan_destroy(None) == 0
+    assert lib.gcg_spmm_csr_f32_planned(None, None, None, None, None, 1, 1, None, 1, None, 0, None, 0, None) == 1
+    assert lib.gcg_scatter_add_rows_f32(-1, None, None, None, 1, 1, None, 1, None) == 1
+    assert lib.gcg_spgemm(1, 1, 1, 0, None, None, None, 0, 0, None, None, None, 0, 0, None, None, None, None, None) == 1
+    assert lib.gcg_spgemm_products(-1, 0, None, None, 0, None, None, None) == 1
+    msg = lib.gcg_last_error().decode()
+    assert msg  # a readable message for the last failure on this thread
+    with pytest.raises(_native.NativeError, match="INVALID_ARG"):
+        _native.call("gcg_spmm_csr_f32", -1, 1, 0, None, None, None, None, 1, 1, None, 1, None, 0, None, 0, None)
