@@ -1,0 +1,62 @@
+"""Parity at BASELINE.json's full sizes (Twitter-US / Twitter-World), through properties
+that do not need a full CPU product: sampled rows against the oracle (the oracle takes a
+row subset), fast == ordered within 1e-5, linearity, and a checksum of row checksums."""
+import numpy as np
+import pytest
+import torch
+
+from graphconvgeo_amd import sparse as gs
+from graphconvgeo_amd.synth import CONFIGS, synthetic_graph
+from oracle import gcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", params=["twitter-us", "twitter-world"])
+def big(request, cuda):
+    cfg = CONFIGS[request.param]
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    Z = torch.randn((cfg.n_nodes, cfg.hidden), generator=g, device=cuda)
+    return cfg, H, A, Z
+
+
+def test_sampled_rows_bitwise(big):
+    cfg, H, A, Z = big
+    Y = gs.spmm(A, Z, mode="ordered")
+    lens = np.diff(H.indptr)
+    rows = np.unique(np.concatenate([
+        np.random.default_rng(0).integers(0, cfg.n_nodes, 2000),
+        np.argsort(lens)[-50:],            # the hubs (longest rows)
+        np.argsort(lens)[:50],             # the shortest rows
+        [0, cfg.n_nodes - 1]]))
+    Zh = Z.cpu().numpy()
+    ref = O.spmm_f32(H, Zh, rows=rows)
+    assert np.array_equal(Y[torch.as_tensor(rows, device=Y.device)].cpu().numpy(), ref)
+
+
+def test_fast_vs_ordered_and_checksums(big):
+    cfg, H, A, Z = big
+    Yo = gs.spmm(A, Z, mode="ordered")
+    Yf = gs.spmm(A, Z, mode="fast")
+    assert float((Yo - Yf).abs().max()) <= 1e-5
+    # checksum of row checksums (float64 on device) vs the sampled oracle's rows
+    cs_o = Yo.double().sum(dim=1)
+    cs_f = Yf.double().sum(dim=1)
+    assert float((cs_o - cs_f).abs().max()) <= 1e-5 * cfg.hidden
+    # row-sum identity of the normalized operator: (H . 1)_i = sum_j H_ij
+    ones = torch.ones((cfg.n_nodes, 4), device=Z.device)
+    h1 = gs.spmm(A, ones, mode="ordered")[:, 0].double().cpu().numpy()
+    rs = np.asarray(H.sum(axis=1, dtype=np.float64)).ravel()
+    # fp32 storage-order sums of up to ~12k positive terms (hub rows sum to ~30): relative bar
+    assert np.all(np.abs(h1 - rs) <= 1e-4 * np.maximum(1.0, rs))
+
+
+def test_linearity(big):
+    cfg, H, A, Z = big
+    g = torch.Generator(device=Z.device).manual_seed(9)
+    Z2 = torch.randn(Z.shape, generator=g, device=Z.device)
+    lhs = gs.spmm(A, Z + Z2)
+    rhs = gs.spmm(A, Z) + gs.spmm(A, Z2)
+    assert float((lhs - rhs).abs().max()) <= 2e-5
