@@ -42,16 +42,37 @@ class LasagneAdam:
         self.t = 0
         self.m = [torch.zeros_like(p) for p in self.params]
         self.v = [torch.zeros_like(p) for p in self.params]
+        # a_t lives on the device so a captured HIP graph reads the current step's value
+        self.a_t = torch.zeros((), dtype=torch.float32, device=self.params[0].device)
 
-    @torch.no_grad()
-    def step(self):
+    def prepare(self):
+        """Host half of a step: t += 1 and the bias-corrected step size (Python double,
+        rounded once to float32 exactly as an eager `a_t * m` would round it)."""
         self.t += 1
         a_t = self.lr * math.sqrt(1 - self.beta2 ** self.t) / (1 - self.beta1 ** self.t)
+        self.a_t.fill_(a_t)
+
+    @torch.no_grad()
+    def apply(self):
+        """Device half of a step (capturable)."""
         for p, m, v in zip(self.params, self.m, self.v):
             g = p.grad
             m.mul_(self.beta1).add_(g, alpha=1 - self.beta1)
             v.mul_(self.beta2).addcmul_(g, g, value=1 - self.beta2)
-            p.sub_(a_t * m / (v.sqrt() + self.eps))
+            p.sub_(self.a_t * m / (v.sqrt() + self.eps))
+
+    def step(self):
+        self.prepare()
+        self.apply()
+
+    def state(self):
+        return {"t": self.t, "m": [x.clone() for x in self.m], "v": [x.clone() for x in self.v]}
+
+    @torch.no_grad()
+    def load_state(self, st):
+        self.t = st["t"]
+        for dst, src in zip(self.m + self.v, st["m"] + st["v"]):
+            dst.copy_(src)
 
     def zero_grad(self):
         for p in self.params:
@@ -65,7 +86,7 @@ class MLPCONV:
                  early_stopping_max_down=100000, loss_name="log", nonlinearity="rectify",
                  dtype="float32", device="cuda", seed: Optional[int] = None, mode: str = "auto",
                  model_file: Optional[str] = None, report_k_epoch: int = 10,
-                 order: str = "reference"):
+                 order: str = "reference", use_graph: bool = False):
         if dtype != "float32":
             raise ValueError("the GPU path computes in float32 (mlpconv.py dtype='float32')")
         if drop_out:
@@ -89,6 +110,7 @@ class MLPCONV:
         self.model_file = model_file
         self.report_k_epoch = report_k_epoch
         self.order = order  # ConvolutionDenseLayer order: reference | propagate_first | auto
+        self.use_graph = use_graph  # replay each epoch's fwd+bwd+adam as one captured HIP graph
         self.history = []
 
     # -- model --------------------------------------------------------------------------
@@ -152,12 +174,11 @@ class MLPCONV:
         y_train = torch.as_tensor(Y[self.train_indices].astype(np.int64), device=self.device)
         y_dev = torch.as_tensor(Y[self.dev_indices].astype(np.int64), device=self.device)
         opt = LasagneAdam(self.params, lr=4e-3, beta1=0.9, beta2=0.999, epsilon=1e-8)
+        self.optimizer = opt
+        train_step = self._make_train_step(opt, y_train)
         best_params, best_val_loss, best_val_acc, n_down = None, math.inf, 0.0, 0
         for n in range(self.n_epochs):
-            opt.zero_grad()
-            loss, acc = self._loss_acc(self.rows["train"], y_train)
-            loss.backward()
-            opt.step()
+            loss, acc = train_step()
             rec = {"epoch": n, "train_loss": float(loss), "train_acc": float(acc)}
             if n % self.report_k_epoch == 0:
                 with torch.no_grad():
@@ -184,6 +205,52 @@ class MLPCONV:
         if self.model_file:
             torch.save([p.detach().cpu() for p in self.params], self.model_file)
         return self
+
+    def _make_train_step(self, opt: LasagneAdam, y_train: torch.Tensor):
+        """One epoch (mlpconv.py:295): eager, or a captured HIP graph replayed per epoch.
+
+        Capture: one eager warm-up step on a side stream builds every lazy resource (launch
+        plans, CSR(X^T), index CSRs, BLAS handles) outside the capture, then parameters and
+        Adam state are restored, so the graph path computes exactly the eager trajectory."""
+        rows = self.rows["train"]
+
+        def eager():
+            opt.zero_grad()
+            loss, acc = self._loss_acc(rows, y_train)
+            loss.backward()
+            opt.step()
+            return loss.detach(), acc
+
+        if not self.use_graph or self.n_epochs == 0:
+            return eager
+        snap_p = [p.detach().clone() for p in self.params]
+        snap_o = opt.state()
+        side = torch.cuda.Stream(self.device)
+        side.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(side):
+            eager()
+        torch.cuda.current_stream(self.device).wait_stream(side)
+        with torch.no_grad():
+            for p, s in zip(self.params, snap_p):
+                p.copy_(s)
+        opt.load_state(snap_o)
+        opt.zero_grad()
+        graph = torch.cuda.CUDAGraph()
+        opt.prepare()  # step 1's a_t, written before capture (and before every replay)
+        opt.t -= 1
+        with torch.cuda.graph(graph):
+            loss, acc = self._loss_acc(rows, y_train)
+            loss.backward()
+            opt.apply()
+        static = (loss.detach(), acc)
+        self._graph = graph
+
+        def replay():
+            opt.prepare()
+            graph.replay()
+            return static
+
+        return replay
 
     def _indices(self, partition):
         if partition not in self.rows:

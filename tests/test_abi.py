@@ -142,3 +142,16 @@ def test_abi_argument_validation_without_gpu(native_lib):
     assert msg  # a readable message for the last failure on this thread
     with pytest.raises(_native.NativeError, match="INVALID_ARG"):
         _native.call("gcg_spmm_csr_f32", -1, 1, 0, None, None, None, None, 1, 1, None, 1, None, 0, None, 0, None)
+
+
+def test_plain_c_consumer(native_lib, tmp_path):
+    """tests/c/abi_consumer.c builds with gcc against include/gcg_spmm.h and links the .so."""
+    from graphconvgeo_amd import _native
+    lib = _native.lib_path()
+    exe = tmp_path / "abi_consumer"
+    src = os.path.join(ROOT, "tests", "c", "abi_consumer.c")
+    subprocess.run(["gcc", "-std=c99", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), src,
+                    lib, f"-Wl,-rpath,{os.path.dirname(lib)}", "-o", str(exe)], check=True)
+    res = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert res.returncode == 0, (res.returncode, res.stdout, res.stderr)
+    assert "abi ok" in res.stdout

@@ -73,3 +73,14 @@ def test_mlpconv_propagate_first_order(cuda):
     got = np.array([h["train_loss"] for h in clf.history])
     ref = np.array([h["train_loss"] for h in hist])
     assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max()), (got, ref)
+
+
+def test_mlpconv_hip_graph_equals_eager(cuda):
+    H, X, Y, train, dev, test, init = problem(n=3000, e=20000, f=200, k=32, c=7)
+    kw = dict(n_epochs=11, hidden_layer_size=32, regul_coefs=(1e-5, 1e-5), init_parameters=init,
+              device=cuda, report_k_epoch=5)
+    a = MLPCONV(**kw).fit(X, train, dev, test, Y, H)
+    b = MLPCONV(use_graph=True, **kw).fit(X, train, dev, test, Y, H)
+    assert [h["train_loss"] for h in a.history] == [h["train_loss"] for h in b.history]
+    for pa, pb in zip(a.get_params(), b.get_params()):
+        assert np.array_equal(pa, pb)  # replayed graph == eager, bit for bit

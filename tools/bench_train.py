@@ -37,6 +37,7 @@ def main():
     ap.add_argument("--nnz-per-row", type=int, default=64)
     ap.add_argument("--mode", default="auto")
     ap.add_argument("--order", default="reference", choices=["reference", "propagate_first", "auto"])
+    ap.add_argument("--graph", action="store_true", help="replay the step as a captured HIP graph")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
@@ -54,17 +55,12 @@ def main():
     test_idx = np.arange(int(0.8 * n), n, dtype=np.int32)
 
     clf = MLPCONV(n_epochs=0, hidden_layer_size=cfg.hidden, device=dev, seed=1, mode=args.mode,
-                  order=args.order)
+                  order=args.order, use_graph=args.graph)
     clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H/X, no epochs
     y_train = torch.as_tensor(Y[train].astype(np.int64), device=dev)
     opt = LasagneAdam(clf.params)
-
-    def step():
-        opt.zero_grad()
-        loss, _acc = clf._loss_acc(clf.rows["train"], y_train)
-        loss.backward()
-        opt.step()
-        return loss
+    clf.n_epochs = 1  # let _make_train_step capture when --graph
+    step = clf._make_train_step(opt, y_train)
 
     for _ in range(args.warmup):
         step()
@@ -87,7 +83,8 @@ def main():
            "nodes": n, "nnz_H": nnzH, "nnz_X": nnzX, "F": cfg.n_features, "K": K, "C": C,
            "train_rows": len(train), "spmm_algorithmic_bytes_per_step": total,
            "spmm_effective_GBps_if_all_time_in_spmm": round(total / (ms * 1e-3) / 1e9, 1),
-           "mode": args.mode, "order": args.order, "data_gen_s": round(t_gen, 1)}
+           "mode": args.mode, "order": args.order, "hip_graph": args.graph,
+           "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
 
