@@ -177,14 +177,14 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
 //   tasks == nullptr : task w = rows of positions [w, w+1)           (plan-less path)
 //   task.w <  0      : rows of positions [task.x, task.y)            (short rows)
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
-template <int VEC, int NCH, int U>
-__global__ __launch_bounds__(kBlock) void spmm_rows_kernel(
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int4* __restrict__ tasks, int n_tasks, const int32_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
     float* __restrict__ ws, int64_t ldws) {
-  const int w = uniform(static_cast<int>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6));
+  const int w = uniform(static_cast<int>(blockIdx.x) * WPB + (threadIdx.x >> 6));
   if (w >= n_tasks) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
@@ -287,15 +287,36 @@ struct LaunchArgs {
   int64_t ldws;
 };
 
+template <int VEC, int NCH, int U, int WPB>
+void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  const dim3 grid((a.n_tasks + WPB - 1) / WPB, n_panels);
+  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
+                     a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
+                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws);
+}
+
+// Experiment knobs (GCG_UNROLL = gathers per lane per batch, GCG_WPB = waves per workgroup),
+// instantiated for the K = 300 variant only; 0 / unset = the defaults below.
+int env_int(const char* name) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : 0;
+}
+
 template <int VEC, int NCH>
 void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   constexpr int kInFlight = 64;  // floats per lane held by the in-flight gather batch
   constexpr int U0 = kInFlight / (VEC * NCH);
   constexpr int U = U0 > 16 ? 16 : (U0 < 2 ? 2 : U0);
-  const dim3 grid((a.n_tasks + kWavesPerBlock - 1) / kWavesPerBlock, n_panels);
-  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U>), grid, dim3(kBlock), 0, stream, a.tasks,
-                     a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y,
-                     a.ldy, a.bias, a.act, a.ws, a.ldws);
+  if constexpr (VEC == 4 && NCH == 2) {
+    static const int u = env_int("GCG_UNROLL"), wpb = env_int("GCG_WPB");
+    if (u == 4) return launch_rows_u<4, 2, 4, kWavesPerBlock>(a, n_panels, stream);
+    if (u == 12) return launch_rows_u<4, 2, 12, kWavesPerBlock>(a, n_panels, stream);
+    if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
+    if (wpb == 1) return launch_rows_u<4, 2, U, 1>(a, n_panels, stream);
+    if (wpb == 2) return launch_rows_u<4, 2, U, 2>(a, n_panels, stream);
+    if (wpb == 8) return launch_rows_u<4, 2, U, 8>(a, n_panels, stream);
+  }
+  launch_rows_u<VEC, NCH, U, kWavesPerBlock>(a, n_panels, stream);
 }
 
 int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
