@@ -84,3 +84,19 @@ def test_mlpconv_hip_graph_equals_eager(cuda):
     assert [h["train_loss"] for h in a.history] == [h["train_loss"] for h in b.history]
     for pa, pb in zip(a.get_params(), b.get_params()):
         assert np.array_equal(pa, pb)  # replayed graph == eager, bit for bit
+
+
+def test_main_mlpconv_call_pattern(cuda):
+    """The exact constructor / fit / accuracy / predict calls of tensormain.main_mlpconv
+    (tensormain.py:232-244), with the import swapped for graphconvgeo_amd's MLPCONV."""
+    H, X, Y, train, dev, test, _init = problem(n=2500, e=15000, f=200, k=24, c=6)
+    regul, hidden_size, batch_size, dropout_coefs, dtype = 1e-6, 24, 500, [0.5, 0.5], "float32"
+    clf = MLPCONV(n_epochs=30, batch_size=batch_size, init_parameters=None, complete_prob=False,
+                  add_hidden=True, regul_coefs=[regul, regul], save_results=False,
+                  hidden_layer_size=hidden_size, drop_out=False, dropout_coefs=dropout_coefs,
+                  early_stopping_max_down=5, loss_name='log', nonlinearity='rectify', dtype=dtype)
+    clf.fit(X, train, dev, test, Y, H)
+    acc = clf.accuracy(dataset_partition='test', y_true=Y[test].astype('int32'))
+    y_pred = clf.predict(dataset_partition='test')
+    assert 0.0 <= acc <= 1.0 and y_pred.shape == (len(test),)
+    assert acc > 1.5 / 6  # learns beyond chance on feature-correlated labels
