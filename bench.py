@@ -82,6 +82,36 @@ def cpu_baseline(H, K: int, budget_s: float) -> dict:
                       f"1 thread on {cpu_model()} ({os.cpu_count()} host cpus)"}
 
 
+def cpu_multicore(H, K: int, budget_s: float) -> dict:
+    """Extra, labelled: torch's CPU CSR x dense on every host thread torch uses (SURVEY.md
+    §8d optional multi-core reference) -- not the reference's executor, which is 1-thread."""
+    import torch as _t
+
+    n = H.shape[0]
+    stop = int(np.searchsorted(H.indptr, min(H.nnz, 8_000_000), side="left"))
+    blk = H[:max(stop, 1)]
+    import warnings
+
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        A = _t.sparse_csr_tensor(_t.from_numpy(blk.indptr.astype(np.int64)),
+                                 _t.from_numpy(blk.indices.astype(np.int64)),
+                                 _t.from_numpy(blk.data), size=blk.shape)
+    Z = _t.randn((n, K), dtype=_t.float32)
+    _t.sparse.mm(A, Z)
+    reps, t_total = 0, 0.0
+    while t_total < budget_s and reps < 50:
+        t0 = time.perf_counter()
+        _t.sparse.mm(A, Z)
+        t_total += time.perf_counter() - t0
+        reps += 1
+    t = t_total / reps
+    return {"value": round(spmm_bytes(blk.shape[0], blk.nnz, K) / t / 1e9, 3), "unit": "GB/s",
+            "cores": _t.get_num_threads(), "kind": "torch.sparse.mm (CPU, multi-thread)",
+            "edges_per_s": round(blk.nnz / t, 1),
+            "sample": f"rows [0, {blk.shape[0]}): {blk.nnz} nnz x K={K}, {reps} reps"}
+
+
 def load_traffic(workload: str, per_launch_bytes: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload."""
     path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
@@ -275,6 +305,10 @@ def main():
         rec["distributed"] = dist_info
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(H, K, args.cpu_budget)
+        try:
+            rec["cpu_multicore"] = cpu_multicore(H, K, min(args.cpu_budget, 5.0))
+        except Exception as exc:  # informational only
+            rec["cpu_multicore"] = {"error": repr(exc)[:200]}
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:
