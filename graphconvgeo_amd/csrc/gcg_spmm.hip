@@ -285,6 +285,7 @@ struct LaunchArgs {
   int act;
   float* ws;
   int64_t ldws;
+  int64_t task_nnz;  // plan task size (0 = plan-less, one row per wave)
 };
 
 template <int VEC, int NCH, int U, int WPB>
@@ -302,21 +303,28 @@ int env_int(const char* name) {
   return e ? std::atoi(e) : 0;
 }
 
+// Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
+// nonzeros). Measured (MI355X, same box, K = 300 variant VEC = 4 / NCH = 2): 192 floats
+// (U = 24, 210 VGPRs, 2 waves/SIMD) vs 64 (U = 8, 92 VGPRs, 5 waves/SIMD): Twitter-World
+// power-law 6.67 vs 6.97 ms, Twitter-US 1.70 vs 1.81 ms, uniform equal; but slower on the
+// small GEOTEXT graph (32-nnz tasks: 39 vs 26 us) and for the narrower variants (K = 64, 128,
+// 129). 256 floats (U = 32) drops to 1 wave/SIMD and halves throughput. So the deep batch is
+// used for the VEC 4 x 2 variant with >= 256-nnz tasks only; GCG_INFLIGHT=64 forces the shallow.
+template <int VEC, int NCH, int INFLIGHT>
+void launch_rows_f(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  constexpr int U0 = INFLIGHT / (VEC * NCH);
+  constexpr int U = U0 > 24 ? 24 : (U0 < 2 ? 2 : U0);
+  launch_rows_u<VEC, NCH, U, kWavesPerBlock>(a, n_panels, stream);
+}
+
 template <int VEC, int NCH>
 void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
-  constexpr int kInFlight = 64;  // floats per lane held by the in-flight gather batch
-  constexpr int U0 = kInFlight / (VEC * NCH);
-  constexpr int U = U0 > 16 ? 16 : (U0 < 2 ? 2 : U0);
   if constexpr (VEC == 4 && NCH == 2) {
-    static const int u = env_int("GCG_UNROLL"), wpb = env_int("GCG_WPB");
-    if (u == 4) return launch_rows_u<4, 2, 4, kWavesPerBlock>(a, n_panels, stream);
-    if (u == 12) return launch_rows_u<4, 2, 12, kWavesPerBlock>(a, n_panels, stream);
+    static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
     if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
-    if (wpb == 1) return launch_rows_u<4, 2, U, 1>(a, n_panels, stream);
-    if (wpb == 2) return launch_rows_u<4, 2, U, 2>(a, n_panels, stream);
-    if (wpb == 8) return launch_rows_u<4, 2, U, 8>(a, n_panels, stream);
+    if (inflight != 64 && a.task_nnz >= 256) return launch_rows_f<4, 2, 192>(a, n_panels, stream);
   }
-  launch_rows_u<VEC, NCH, U, kWavesPerBlock>(a, n_panels, stream);
+  launch_rows_f<VEC, NCH, 64>(a, n_panels, stream);
 }
 
 int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
@@ -510,7 +518,7 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz, const i
   if (nnz > 0 && (indices == nullptr || vals == nullptr)) return fail(GCG_ERR_INVALID_ARG, "indices/vals NULL");
   if (n_out == 0 || K == 0) return GCG_OK;
   LaunchArgs a{nullptr, int(n_out), indptr, indices, vals, out_rows, Z, ldz, int(K), Y, ldy,
-               bias, act, nullptr, 0};
+               bias, act, nullptr, 0, 0};
   return launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, nullptr, 0),
                      static_cast<hipStream_t>(stream));
 }
@@ -642,7 +650,7 @@ gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* in
   float* ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
-               Y, ldy, bias, act, ws, ldws};
+               Y, ldy, bias, act, ws, ldws, plan->task_nnz};
   if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
   if (plan->n_long > 0) {
     const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);
