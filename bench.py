@@ -151,6 +151,8 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
+    ap.add_argument("--no-alternatives", dest="alternatives", action="store_false",
+                    help="N > 1: skip timing the feature-parallel alternative")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned (all-gather) path even at N = 1")
     args = ap.parse_args()
@@ -287,6 +289,24 @@ def main():
                      "nnz_local": part.nnz_local, "block_rows": part.block_rows,
                      "spmm_only_aggregate_GBps": round(B / (t_sp * 1e-3) / 1e9, 1)}
 
+    # Alternative strategy measured in the same run (N > 1): H replicated, Z split by columns,
+    # no exchange (distributed.FeatureParallelSpMM). Reported beside the row-partitioned value.
+    alt = None
+    if world > 1 and args.alternatives:
+        from graphconvgeo_amd.distributed import FeatureParallelSpMM
+        fp = FeatureParallelSpMM(H, rank, world, dev, K)
+        Zc = torch.randn((N, fp.width), generator=gen, device=dev, dtype=torch.float32)
+        Yc = gs.empty_dense(N, fp.width, dev)
+        fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
+        for _ in range(args.warmup):
+            fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
+        t_fp = timed(lambda: fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz), args.steps)
+        alt = {"feature_parallel": {"ms_per_step": round(t_fp, 4),
+                                    "value": round(B / (t_fp * 1e-3) / 1e9, 1), "unit": "GB/s",
+                                    "columns_per_gpu": fp.width, "exchange": "none",
+                                    "note": "H replicated (0.34 GB), Z/Y split by columns"}}
+        del fp, Zc, Yc
+
     value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
@@ -303,6 +323,8 @@ def main():
         rec["roofline"] = roofline
     if dist_info:
         rec["distributed"] = dist_info
+    if alt:
+        rec["alternatives"] = alt
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         rec["cpu_baseline"] = cpu_baseline(H, K, args.cpu_budget)
         try:

@@ -102,3 +102,18 @@ def test_halo_layout_and_auto_choice():
         assert np.array_equal(O.spmm_f32(p.local_host, operand), O.spmm_f32(H, Z)[p.start:p.stop])
     dense = RowPartitionedCSR(H, 0, 2, "cpu", local_spmm=_oracle_spmm)  # halo ~100% -> allgather
     assert dense.halo_fraction > 0.9 and dense.exchange == "allgather"
+
+
+def test_feature_parallel_columns_concatenate_to_full():
+    from graphconvgeo_amd.distributed import FeatureParallelSpMM, feature_partition
+    from oracle import gcn_oracle as O
+    assert feature_partition(300, 8)[0] == (0, 40) and feature_partition(300, 8)[-1] == (280, 300)
+    assert feature_partition(10, 4) == [(0, 4), (4, 8), (8, 10), (10, 10)]
+    H = synthetic_graph(2000, 12000)
+    Z = np.random.default_rng(3).standard_normal((2000, 30)).astype(np.float32)
+    ref = O.spmm_f32(H, Z)
+    parts = []
+    for r in range(3):
+        fp = FeatureParallelSpMM(H, r, 3, "cpu", 30, local_spmm=_oracle_spmm)
+        parts.append(fp.spmm(torch.from_numpy(np.ascontiguousarray(Z[:, fp.c0:fp.c1]))).numpy())
+    assert np.array_equal(np.concatenate(parts, axis=1), ref)  # column-local: bitwise
