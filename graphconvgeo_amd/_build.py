@@ -11,14 +11,19 @@ import subprocess
 
 PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
-SRC = os.path.join(PKG_DIR, "csrc", "gcg_spmm.hip")
+CSRC = os.path.join(PKG_DIR, "csrc")
+# Translation units of libgcg_spmm.so: SpMM kernels + planner, CSR utilities, graph build,
+# SpGEMM, error/version helpers. Compiled in parallel, linked into one shared library.
+SOURCES = [os.path.join(CSRC, f) for f in
+           ("spmm.hip", "csr_ops.hip", "graph_build.hip", "spgemm.hip", "errors.cpp")]
+INTERNAL_HEADERS = [os.path.join(CSRC, h) for h in ("common.h", "index_kernels.h")]
 HEADER = os.path.join(REPO_DIR, "include", "gcg_spmm.h")
 LIB = os.path.join(PKG_DIR, "libgcg_spmm.so")
 ARCH = os.environ.get("GCG_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: every product and sum is rounded separately, as scipy's csr_matvecs does.
-HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", "-shared",
-               f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-command-line-argument"]
+HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}",
+               "-Wall", "-Wno-unused-command-line-argument"]
 
 
 def _hipcc() -> str:
@@ -32,21 +37,42 @@ def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (SRC, HEADER, __file__))
+    return any(os.path.getmtime(p) > t for p in (*SOURCES, *INTERNAL_HEADERS, HEADER, __file__))
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
-    """Compile csrc/gcg_spmm.hip into libgcg_spmm.so for gfx950. Returns the path."""
+    """Compile csrc/* for gfx950 and link libgcg_spmm.so (in-tree). Returns the path."""
     if not force and not needs_build():
         return LIB
-    tmp = LIB + ".tmp"
-    cmd = [_hipcc(), *HIPCC_FLAGS, "-o", tmp, SRC]
-    if verbose:
-        print(" ".join(cmd))
-    res = subprocess.run(cmd, capture_output=True, text=True)
-    if res.returncode != 0:
-        raise RuntimeError(f"hipcc failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
-    os.replace(tmp, LIB)
+    import concurrent.futures as cf
+    import tempfile
+
+    hipcc = _hipcc()
+    with tempfile.TemporaryDirectory(prefix="gcg_build_") as tmpd:
+        objs = [os.path.join(tmpd, os.path.basename(src) + ".o") for src in SOURCES]
+
+        def compile_one(src_obj):
+            src, obj = src_obj
+            cmd = [hipcc, *HIPCC_FLAGS, "-c", "-o", obj, src]
+            if src.endswith(".cpp"):
+                cmd = [hipcc, "-x", "hip", *cmd[1:]]
+            if verbose:
+                print(" ".join(cmd))
+            return subprocess.run(cmd, capture_output=True, text=True), src
+
+        workers = min(len(SOURCES), max(1, (os.cpu_count() or 2)), 8)
+        with cf.ThreadPoolExecutor(max_workers=workers) as ex:
+            for res, src in ex.map(compile_one, zip(SOURCES, objs)):
+                if res.returncode != 0:
+                    raise RuntimeError(f"hipcc failed on {src} ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+        tmp = LIB + ".tmp"
+        cmd = [hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", "-o", tmp, *objs]
+        if verbose:
+            print(" ".join(cmd))
+        res = subprocess.run(cmd, capture_output=True, text=True)
+        if res.returncode != 0:
+            raise RuntimeError(f"link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
+        os.replace(tmp, LIB)
     return LIB
 
 

@@ -1,0 +1,622 @@
+// spmm.hip -- MI355X (gfx950 / CDNA4) CSR x dense SpMM for the graphconvgeo GCN hot path.
+//
+// Implements the SpMM part of include/gcg_spmm.h. The reference computes Y = act(H . Z + b) with
+// theano.sparse.dot (mlpconv.py:71,73,90) on the host CPU via scipy `csr_matvecs`;
+// here the product is a memory-bound row gather on the GPU:
+//
+//   * One 64-lane wave owns one output row at a time. Lanes span the dense width K
+//     in VEC-float vectors (16-byte dwordx4 loads when K, ldz, ldy and the pointers
+//     allow), so one nonzero costs one coalesced read of a whole Z row (1200 B at
+//     K = 300: 64 lanes x 16 B + 11 lanes x 16 B).
+//   * The row's (column, value) pairs are wave-uniform: they are read through the
+//     scalar unit (s_load) and the Z row base is an SGPR, so there is no per-lane
+//     index traffic and no divergence.
+//   * U nonzeros are gathered per batch before any is consumed (U x row bytes in
+//     flight per wave) and then accumulated in storage order, mul and add rounded
+//     separately (-ffp-contract=off): bitwise scipy float32.
+//   * Widths beyond one panel (64 lanes x VEC x NCH <= 512 floats) are split into
+//     column panels on grid.y; each panel re-reads only the 8-byte (col, val) stream.
+//   * Load balance (power-law degrees, data.py:245-249 co-mention cliques): the plan
+//     groups consecutive rows into tasks of ~task_nnz nonzeros, and splits longer rows
+//     into segments whose partial sums go to a workspace; a fix-up kernel adds the
+//     segments of each split row in order and applies the epilogue.
+//   * Epilogue fused: + bias (mlpconv.py:75-76,92-93), rectify = 0.5*(x+|x|) as
+//     Theano's nnet.relu computes it (mlpconv.py:77 via lasagne.nonlinearities.rectify),
+//     and the target_indices row subset (mlpconv.py:94) via out_rows.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <new>
+#include <utility>
+#include <vector>
+
+#include "common.h"
+
+using namespace gcg;
+
+namespace {
+
+constexpr int kPanelMax = 512;  // floats per column panel
+constexpr int64_t kDefaultTaskNnz = 512;
+constexpr int64_t kRowCost = 2;  // planner: per-row overhead in nonzero-equivalents
+
+// ------------------------------------------------------------------------------------
+// Vector helpers. Explicit per-component arithmetic keeps the rounding sequence
+// exactly acc = acc + (v * z) per element.
+// ------------------------------------------------------------------------------------
+template <int VEC>
+struct Vec {
+  float x[VEC];
+};
+
+template <int VEC>
+__device__ __forceinline__ Vec<VEC> load_vec(const float* __restrict__ p) {
+  Vec<VEC> r;
+  if constexpr (VEC == 4) {
+    const float4 t = *reinterpret_cast<const float4*>(p);
+    r.x[0] = t.x; r.x[1] = t.y; r.x[2] = t.z; r.x[3] = t.w;
+  } else if constexpr (VEC == 2) {
+    const float2 t = *reinterpret_cast<const float2*>(p);
+    r.x[0] = t.x; r.x[1] = t.y;
+  } else {
+    r.x[0] = *p;
+  }
+  return r;
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_vec(float* __restrict__ p, const Vec<VEC>& v) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<float4*>(p) = make_float4(v.x[0], v.x[1], v.x[2], v.x[3]);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<float2*>(p) = make_float2(v.x[0], v.x[1]);
+  } else {
+    *p = v.x[0];
+  }
+}
+
+__device__ __forceinline__ float apply_act(float y, int act) {
+  // lasagne.nonlinearities.rectify -> theano.tensor.nnet.relu(x) = 0.5 * (x + abs(x))
+  return act == GCG_ACT_RELU ? 0.5f * (y + fabsf(y)) : y;
+}
+
+// Accumulate nonzeros [s, e) of one row into acc, storage order, U gathers in flight.
+template <int VEC, int NCH, int U>
+__device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __restrict__ indices,
+                                                 const float* __restrict__ vals,
+                                                 const float* __restrict__ Z, int64_t ldz,
+                                                 const int (&col)[NCH], Vec<VEC> (&acc)[NCH]) {
+  // `col` is pre-clamped for lanes past K (they re-read a column of the same row, which
+  // coalesces with lane 0's line): no exec-mask branches, so hipcc can count vmcnt.
+  int j = s;
+  for (; j + U <= e; j += U) {
+    int c[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = indices[j + u];
+      v[u] = vals[j + u];
+    }
+    Vec<VEC> z[U][NCH];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k)
+        z[u][k] = load_vec<VEC>(zrow + col[k]);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+  }
+  const int rem = e - j;  // wave-uniform, < U
+  if (rem > 0) {
+    int c[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (u < rem) {
+        c[u] = indices[j + u];
+        v[u] = vals[j + u];
+      }
+    Vec<VEC> z[U][NCH];
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (u < rem) {
+        const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+          z[u][k] = load_vec<VEC>(zrow + col[k]);
+      }
+#pragma unroll
+    for (int u = 0; u < U - 1; ++u)
+      if (u < rem)
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+#pragma unroll
+          for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+  }
+}
+
+// Main kernel. One wave per task; grid.y = column panel.
+//   tasks == nullptr : task w = rows of positions [w, w+1)           (plan-less path)
+//   task.w <  0      : rows of positions [task.x, task.y)            (short rows)
+//   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
+    const int4* __restrict__ tasks, int n_tasks, const int32_t* __restrict__ indptr,
+    const int32_t* __restrict__ indices, const float* __restrict__ vals,
+    const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
+    float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
+    float* __restrict__ ws, int64_t ldws) {
+  const int w = uniform(static_cast<int>(blockIdx.x) * WPB + (threadIdx.x >> 6));
+  if (w >= n_tasks) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
+
+  int col[NCH], gcol[NCH];  // output column / clamped gather column
+  bool on[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    col[k] = panel0 + (k * kWave + lane) * VEC;
+    on[k] = col[k] < K;
+    gcol[k] = on[k] ? col[k] : panel0;
+  }
+
+  int4 t;
+  if (tasks != nullptr) {
+    t = tasks[w];
+    t.x = uniform(t.x); t.y = uniform(t.y); t.z = uniform(t.z); t.w = uniform(t.w);
+  } else {
+    t = make_int4(w, w + 1, -1, -1);
+  }
+
+  Vec<VEC> acc[NCH];
+  if (t.w >= 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[k].x[q] = 0.0f;
+    accumulate_range<VEC, NCH, U>(t.y, t.z, indices, vals, Z, ldz, gcol, acc);
+    float* dst = ws + static_cast<int64_t>(t.w) * ldws;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+      if (on[k]) store_vec<VEC>(dst + col[k], acc[k]);
+    return;
+  }
+
+  for (int p = t.x; p < t.y; ++p) {
+    const int r = out_rows ? uniform(out_rows[p]) : p;
+    const int s = uniform(indptr[r]);
+    const int e = uniform(indptr[r + 1]);
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[k].x[q] = 0.0f;
+    accumulate_range<VEC, NCH, U>(s, e, indices, vals, Z, ldz, gcol, acc);
+    float* yrow = Y + static_cast<int64_t>(p) * ldy;
+#pragma unroll
+    for (int k = 0; k < NCH; ++k) {
+      if (!on[k]) continue;
+      if (bias != nullptr) {
+        const Vec<VEC> b = load_vec<VEC>(bias + col[k]);
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + b.x[q];
+      }
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) acc[k].x[q] = apply_act(acc[k].x[q], act);
+      store_vec<VEC>(yrow + col[k], acc[k]);
+    }
+  }
+}
+
+// Fix-up for split rows: Y[p] = act(sum_{s in slots, in order} ws[s] + bias).
+// One wave per (split row, 64-column strip).
+__global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(const int4* __restrict__ longs,
+                                                            int n_long,
+                                                            const float* __restrict__ ws,
+                                                            int64_t ldws, int K,
+                                                            float* __restrict__ Y, int64_t ldy,
+                                                            const float* __restrict__ bias,
+                                                            int act) {
+  const int w = uniform(static_cast<int>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6));
+  if (w >= n_long) return;
+  const int c = static_cast<int>(blockIdx.y) * kWave + (threadIdx.x & (kWave - 1));
+  if (c >= K) return;
+  const int4 L = longs[w];
+  const float* src = ws + static_cast<int64_t>(L.y) * ldws + c;
+  float acc = src[0];
+  for (int s = 1; s < L.z; ++s) acc = acc + src[static_cast<int64_t>(s) * ldws];
+  if (bias != nullptr) acc = acc + bias[c];
+  Y[static_cast<int64_t>(L.x) * ldy + c] = apply_act(acc, act);
+}
+
+// ------------------------------------------------------------------------------------
+// Launch dispatch: pick VEC (vector width) and NCH (vectors per lane per panel).
+// ------------------------------------------------------------------------------------
+struct LaunchArgs {
+  const int4* tasks;
+  int n_tasks;
+  const int32_t* indptr;
+  const int32_t* indices;
+  const float* vals;
+  const int32_t* out_rows;
+  const float* Z;
+  int64_t ldz;
+  int K;
+  float* Y;
+  int64_t ldy;
+  const float* bias;
+  int act;
+  float* ws;
+  int64_t ldws;
+  int64_t task_nnz;  // plan task size (0 = plan-less, one row per wave)
+};
+
+template <int VEC, int NCH, int U, int WPB>
+void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  const dim3 grid((a.n_tasks + WPB - 1) / WPB, n_panels);
+  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
+                     a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
+                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws);
+}
+
+// Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
+// nonzeros). Measured (MI355X, same box, K = 300 variant VEC = 4 / NCH = 2): 192 floats
+// (U = 24, 210 VGPRs, 2 waves/SIMD) vs 64 (U = 8, 92 VGPRs, 5 waves/SIMD): Twitter-World
+// power-law 6.67 vs 6.97 ms, Twitter-US 1.70 vs 1.81 ms, uniform equal; but slower on the
+// small GEOTEXT graph (32-nnz tasks: 39 vs 26 us) and for the narrower variants (K = 64, 128,
+// 129). 256 floats (U = 32) drops to 1 wave/SIMD and halves throughput. So the deep batch is
+// used for the VEC 4 x 2 variant with >= 256-nnz tasks only; GCG_INFLIGHT=64 forces the shallow.
+template <int VEC, int NCH, int INFLIGHT>
+void launch_rows_f(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  constexpr int U0 = INFLIGHT / (VEC * NCH);
+  constexpr int U = U0 > 24 ? 24 : (U0 < 2 ? 2 : U0);
+  launch_rows_u<VEC, NCH, U, kWavesPerBlock>(a, n_panels, stream);
+}
+
+template <int VEC, int NCH>
+void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  if constexpr (VEC == 4 && NCH == 2) {
+    static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
+    if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
+    if (inflight != 64 && a.task_nnz >= 256) return launch_rows_f<4, 2, 192>(a, n_panels, stream);
+  }
+  launch_rows_f<VEC, NCH, 64>(a, n_panels, stream);
+}
+
+int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
+             const float* bias, const float* ws, int64_t ldws) {
+  for (int vec : {4, 2}) {
+    const size_t bytes = sizeof(float) * vec;
+    if (K % vec == 0 && ldz % vec == 0 && ldy % vec == 0 && aligned(Z, bytes) &&
+        aligned(Y, bytes) && (bias == nullptr || aligned(bias, bytes)) &&
+        (ws == nullptr || (aligned(ws, bytes) && ldws % vec == 0)))
+      return vec;
+  }
+  return 1;
+}
+
+// Returns panel width (floats) and launches.
+int panel_override() {
+  static const int v = [] {
+    const char* e = std::getenv("GCG_PANEL");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
+  const int64_t K = a.K;
+  const int req = panel_override();  // experiment knob: panel width in floats
+  if (req > 0)
+    while (vec > 1 && kWave * vec > req) vec /= 2;
+  const int per_chunk = kWave * vec;
+  const int nch_max = req > 0 ? std::max(1, std::min(kPanelMax, req) / per_chunk) : kPanelMax / per_chunk;
+  int nch = static_cast<int>((K + per_chunk - 1) / per_chunk);
+  if (nch > nch_max) nch = nch_max;
+  if (nch < 1) nch = 1;
+  const int panel = per_chunk * nch;
+  const int n_panels = static_cast<int>((K + panel - 1) / panel);
+  if (a.n_tasks <= 0 || K <= 0) return GCG_OK;
+  switch (vec * 16 + nch) {
+    case 4 * 16 + 1: launch_rows<4, 1>(a, n_panels, stream); break;
+    case 4 * 16 + 2: launch_rows<4, 2>(a, n_panels, stream); break;
+    case 2 * 16 + 1: launch_rows<2, 1>(a, n_panels, stream); break;
+    case 2 * 16 + 2: launch_rows<2, 2>(a, n_panels, stream); break;
+    case 2 * 16 + 3: launch_rows<2, 3>(a, n_panels, stream); break;
+    case 2 * 16 + 4: launch_rows<2, 4>(a, n_panels, stream); break;
+    case 1 * 16 + 1: launch_rows<1, 1>(a, n_panels, stream); break;
+    case 1 * 16 + 2: launch_rows<1, 2>(a, n_panels, stream); break;
+    case 1 * 16 + 3: launch_rows<1, 3>(a, n_panels, stream); break;
+    case 1 * 16 + 4: launch_rows<1, 4>(a, n_panels, stream); break;
+    case 1 * 16 + 5: launch_rows<1, 5>(a, n_panels, stream); break;
+    case 1 * 16 + 6: launch_rows<1, 6>(a, n_panels, stream); break;
+    case 1 * 16 + 7: launch_rows<1, 7>(a, n_panels, stream); break;
+    case 1 * 16 + 8: launch_rows<1, 8>(a, n_panels, stream); break;
+    default: return fail(GCG_ERR_INVALID_ARG, "internal: no kernel for vec=%d nch=%d", vec, nch);
+  }
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+gcg_status check_dense(const float* Z, int64_t ldz, float* Y, int64_t ldy, int64_t K,
+                       const float* bias, int act) {
+  if (K < 0 || K > (int64_t{1} << 30)) return fail(GCG_ERR_INVALID_ARG, "bad K=%lld", (long long)K);
+  if (K > 0 && (Z == nullptr || Y == nullptr)) return fail(GCG_ERR_INVALID_ARG, "Z or Y is NULL");
+  if (ldz < K || ldy < K) return fail(GCG_ERR_INVALID_ARG, "ldz=%lld / ldy=%lld < K=%lld",
+                                      (long long)ldz, (long long)ldy, (long long)K);
+  if (!aligned(Z, 4) || !aligned(Y, 4) || (bias && !aligned(bias, 4)))
+    return fail(GCG_ERR_MISALIGNED, "Z/Y/bias not 4-byte aligned");
+  if (act != GCG_ACT_NONE && act != GCG_ACT_RELU) return fail(GCG_ERR_INVALID_ARG, "bad act=%d", act);
+  return GCG_OK;
+}
+
+// ------------------------------------------------------------------------------------
+// Host planner.
+// ------------------------------------------------------------------------------------
+struct HostPlan {
+  std::vector<int32_t> tasks;  // quadruples
+  std::vector<int32_t> longs;  // quadruples
+  int64_t n_slots = 0;
+  int64_t max_task_nnz = 0;
+};
+
+// Default task size: 512 nonzeros, smaller on small graphs so the launch still has
+// >= ~8k waves (256 CUs x 32 waves) to spread; never below 32.
+int64_t default_task_nnz(int64_t nnz) {
+  int64_t w = nnz / 8192;
+  return w < 32 ? 32 : (w > kDefaultTaskNnz ? kDefaultTaskNnz : w);
+}
+
+gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t* out_rows,
+                           int64_t n_out, int64_t task_nnz, int ordered, HostPlan* hp) {
+  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows]);
+  if (indptr[0] != 0) return fail(GCG_ERR_BAD_CSR, "indptr[0] = %d != 0", indptr[0]);
+  for (int64_t r = 0; r < n_rows; ++r)
+    if (indptr[r + 1] < indptr[r]) return fail(GCG_ERR_BAD_CSR, "indptr decreases at row %lld", (long long)r);
+  hp->tasks.clear();
+  hp->longs.clear();
+  hp->n_slots = 0;
+  hp->max_task_nnz = 0;
+  std::vector<int32_t> seg_tasks;
+  std::vector<std::pair<int64_t, int64_t>> long_rows;  // (nnz, position), ordered mode
+  int64_t cur_begin = -1, cur_cost = 0, cur_nnz = 0;
+  auto close = [&](int64_t end) {
+    if (cur_begin >= 0) {
+      hp->tasks.insert(hp->tasks.end(), {int32_t(cur_begin), int32_t(end), -1, -1});
+      hp->max_task_nnz = std::max(hp->max_task_nnz, cur_nnz);
+    }
+    cur_begin = -1;
+    cur_cost = 0;
+    cur_nnz = 0;
+  };
+  for (int64_t p = 0; p < n_out; ++p) {
+    const int64_t r = out_rows ? out_rows[p] : p;
+    if (r < 0 || r >= n_rows) return fail(GCG_ERR_INVALID_ARG, "out_rows[%lld]=%lld out of range", (long long)p, (long long)r);
+    const int64_t s = indptr[r], e = indptr[r + 1], len = e - s;
+    if (!ordered && len > task_nnz) {
+      close(p);
+      const int64_t nseg = (len + task_nnz - 1) / task_nnz;
+      // Equal-sized segments (differ by at most one nonzero).
+      hp->longs.insert(hp->longs.end(), {int32_t(p), int32_t(hp->n_slots), int32_t(nseg), 0});
+      for (int64_t k = 0; k < nseg; ++k) {
+        const int64_t b = s + (len * k) / nseg, f = s + (len * (k + 1)) / nseg;
+        seg_tasks.insert(seg_tasks.end(), {int32_t(p), int32_t(b), int32_t(f), int32_t(hp->n_slots + k)});
+        hp->max_task_nnz = std::max(hp->max_task_nnz, f - b);
+      }
+      hp->n_slots += nseg;
+      continue;
+    }
+    if (ordered && len > task_nnz) {
+      // Unsplittable long row (bitwise mode): its own task, scheduled first (LPT) so the
+      // serial tail of a hub row overlaps the bulk instead of ending the launch.
+      close(p);
+      long_rows.push_back({len, p});
+      continue;
+    }
+    const int64_t cost = len + kRowCost;
+    if (cur_begin >= 0 && cur_cost + cost > task_nnz) close(p);
+    if (cur_begin < 0) cur_begin = p;
+    cur_cost += cost;
+    cur_nnz += len;
+  }
+  close(n_out);
+  // Longest work first: unsplit long rows (ordered mode) by descending length, then the
+  // segments of split rows, then the short-row tasks in row order.
+  std::stable_sort(long_rows.begin(), long_rows.end(),
+                   [](const std::pair<int64_t, int64_t>& a, const std::pair<int64_t, int64_t>& b) {
+                     return a.first > b.first;
+                   });
+  std::vector<int32_t> head;
+  head.reserve(long_rows.size() * 4 + seg_tasks.size());
+  for (const auto& lr : long_rows) {
+    head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -1, -1});
+    hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
+  }
+  head.insert(head.end(), seg_tasks.begin(), seg_tasks.end());
+  hp->tasks.insert(hp->tasks.begin(), head.begin(), head.end());
+  if (hp->tasks.size() / 4 > static_cast<size_t>(INT32_MAX)) return fail(GCG_ERR_INVALID_ARG, "too many tasks");
+  return GCG_OK;
+}
+
+}  // namespace
+
+// ------------------------------------------------------------------------------------
+struct gcg_spmm_plan {
+  int64_t n_rows = 0, n_cols = 0, nnz = 0, n_out = 0;
+  int ordered = 0;
+  int64_t task_nnz = 0;
+  int n_tasks = 0, n_long = 0;
+  int64_t n_slots = 0, max_task_nnz = 0;
+  int4* tasks = nullptr;     // device
+  int4* longs = nullptr;     // device
+  int32_t* out_rows = nullptr;  // device copy (nullptr = identity)
+};
+
+extern "C" {
+
+gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz, const int32_t* indptr,
+                            const int32_t* indices, const float* vals, const float* Z,
+                            int64_t ldz, int64_t K, float* Y, int64_t ldy, const float* bias,
+                            int act, const int32_t* out_rows, int64_t n_out,
+                            gcg_stream_t stream) {
+  if (n_rows < 0 || n_cols < 0 || nnz < 0 || n_rows > INT32_MAX || nnz > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "bad CSR shape n_rows=%lld n_cols=%lld nnz=%lld",
+                (long long)n_rows, (long long)n_cols, (long long)nnz);
+  if (out_rows == nullptr) n_out = n_rows;
+  if (n_out < 0 || n_out > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "bad n_out=%lld", (long long)n_out);
+  if (gcg_status st = check_dense(Z, ldz, Y, ldy, K, bias, act)) return st;
+  if (n_out > 0 && indptr == nullptr) return fail(GCG_ERR_INVALID_ARG, "indptr is NULL");
+  if (nnz > 0 && (indices == nullptr || vals == nullptr)) return fail(GCG_ERR_INVALID_ARG, "indices/vals NULL");
+  if (n_out == 0 || K == 0) return GCG_OK;
+  LaunchArgs a{nullptr, int(n_out), indptr, indices, vals, out_rows, Z, ldz, int(K), Y, ldy,
+               bias, act, nullptr, 0, 0};
+  return launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, nullptr, 0),
+                     static_cast<hipStream_t>(stream));
+}
+
+gcg_status gcg_spmm_plan_host(int64_t n_rows, const int32_t* indptr_host,
+                              const int32_t* out_rows_host, int64_t n_out, int64_t task_nnz,
+                              int ordered, int32_t* tasks_host, int64_t tasks_cap,
+                              int64_t* n_tasks, int32_t* long_host, int64_t long_cap,
+                              int64_t* n_long, int64_t* n_slots) {
+  if (n_rows < 0 || indptr_host == nullptr) return fail(GCG_ERR_INVALID_ARG, "bad n_rows/indptr");
+  if (out_rows_host == nullptr) n_out = n_rows;
+  HostPlan hp;
+  try {
+    if (gcg_status st = build_host_plan(n_rows, indptr_host, out_rows_host, n_out, task_nnz, ordered, &hp)) return st;
+  } catch (const std::bad_alloc&) {
+    return fail(GCG_ERR_ALLOC, "host allocation failed");
+  }
+  const int64_t nt = hp.tasks.size() / 4, nl = hp.longs.size() / 4;
+  if (n_tasks) *n_tasks = nt;
+  if (n_long) *n_long = nl;
+  if (n_slots) *n_slots = hp.n_slots;
+  if (tasks_host) {
+    if (tasks_cap < nt) return fail(GCG_ERR_INVALID_ARG, "tasks_cap %lld < %lld", (long long)tasks_cap, (long long)nt);
+    std::memcpy(tasks_host, hp.tasks.data(), hp.tasks.size() * sizeof(int32_t));
+  }
+  if (long_host) {
+    if (long_cap < nl) return fail(GCG_ERR_INVALID_ARG, "long_cap %lld < %lld", (long long)long_cap, (long long)nl);
+    std::memcpy(long_host, hp.longs.data(), hp.longs.size() * sizeof(int32_t));
+  }
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_cols,
+                                int64_t nnz, const int32_t* indptr, const int32_t* out_rows,
+                                int64_t n_out, int64_t task_nnz, int ordered,
+                                gcg_stream_t stream) {
+  if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
+  *plan = nullptr;
+  if (n_rows < 0 || n_cols < 0 || nnz < 0 || n_rows > INT32_MAX - 1 || nnz > INT32_MAX || indptr == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "bad CSR shape");
+  if (out_rows == nullptr) n_out = n_rows;
+  if (n_out < 0 || n_out > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "bad n_out");
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  std::vector<int32_t> h_indptr, h_rows;
+  HostPlan hp;
+  try {
+    h_indptr.resize(n_rows + 1);
+    if (out_rows) h_rows.resize(n_out);
+  } catch (const std::bad_alloc&) {
+    return fail(GCG_ERR_ALLOC, "host allocation failed");
+  }
+  GCG_HIP_CHECK(hipMemcpyAsync(h_indptr.data(), indptr, (n_rows + 1) * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  if (out_rows && n_out > 0)
+    GCG_HIP_CHECK(hipMemcpyAsync(h_rows.data(), out_rows, n_out * sizeof(int32_t), hipMemcpyDeviceToHost, st));
+  GCG_HIP_CHECK(hipStreamSynchronize(st));
+  if (h_indptr[n_rows] != nnz)
+    return fail(GCG_ERR_BAD_CSR, "indptr[n_rows]=%d != nnz=%lld", h_indptr[n_rows], (long long)nnz);
+  if (gcg_status s = build_host_plan(n_rows, h_indptr.data(), out_rows ? h_rows.data() : nullptr,
+                                     n_out, task_nnz, ordered, &hp))
+    return s;
+  gcg_spmm_plan* p = new (std::nothrow) gcg_spmm_plan();
+  if (p == nullptr) return fail(GCG_ERR_ALLOC, "plan allocation failed");
+  p->n_rows = n_rows; p->n_cols = n_cols; p->nnz = nnz; p->n_out = n_out;
+  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz);
+  p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
+  p->n_long = static_cast<int>(hp.longs.size() / 4);
+  p->n_slots = hp.n_slots;
+  p->max_task_nnz = hp.max_task_nnz;
+  auto cleanup = [&]() { gcg_spmm_plan_destroy(p); };
+  hipError_t e = hipSuccess;
+  if (p->n_tasks > 0) e = hipMalloc(&p->tasks, hp.tasks.size() * sizeof(int32_t));
+  if (e == hipSuccess && p->n_long > 0) e = hipMalloc(&p->longs, hp.longs.size() * sizeof(int32_t));
+  if (e == hipSuccess && out_rows && n_out > 0) e = hipMalloc(&p->out_rows, n_out * sizeof(int32_t));
+  if (e != hipSuccess) { cleanup(); return fail(GCG_ERR_ALLOC, "hipMalloc: %s", hipGetErrorString(e)); }
+  if (p->n_tasks > 0) e = hipMemcpyAsync(p->tasks, hp.tasks.data(), hp.tasks.size() * sizeof(int32_t), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && p->n_long > 0) e = hipMemcpyAsync(p->longs, hp.longs.data(), hp.longs.size() * sizeof(int32_t), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess && p->out_rows) e = hipMemcpyAsync(p->out_rows, h_rows.data(), n_out * sizeof(int32_t), hipMemcpyHostToDevice, st);
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  if (e != hipSuccess) { cleanup(); return fail(GCG_ERR_HIP, "plan upload: %s", hipGetErrorString(e)); }
+  *plan = p;
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_plan_destroy(gcg_spmm_plan* plan) {
+  if (plan == nullptr) return GCG_OK;
+  hipError_t e1 = plan->tasks ? hipFree(plan->tasks) : hipSuccess;
+  hipError_t e2 = plan->longs ? hipFree(plan->longs) : hipSuccess;
+  hipError_t e3 = plan->out_rows ? hipFree(plan->out_rows) : hipSuccess;
+  delete plan;
+  if (e1 != hipSuccess || e2 != hipSuccess || e3 != hipSuccess)
+    return fail(GCG_ERR_HIP, "hipFree failed in plan destroy");
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_plan_workspace_bytes(const gcg_spmm_plan* plan, int64_t K, size_t* bytes) {
+  if (plan == nullptr || bytes == nullptr || K < 0) return fail(GCG_ERR_INVALID_ARG, "bad args");
+  // Row stride rounded up to 4 floats so the workspace never forces a narrower vector width.
+  const int64_t ldws = (K + 3) & ~int64_t{3};
+  *bytes = static_cast<size_t>(plan->n_slots) * ldws * sizeof(float);
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64_t* n_long_rows,
+                              int64_t* n_segments, int64_t* max_task_nnz) {
+  if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
+  if (n_tasks) *n_tasks = plan->n_tasks;
+  if (n_long_rows) *n_long_rows = plan->n_long;
+  if (n_segments) *n_segments = plan->n_slots;
+  if (max_task_nnz) *max_task_nnz = plan->max_task_nnz;
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                    const int32_t* indices, const float* vals, const float* Z,
+                                    int64_t ldz, int64_t K, float* Y, int64_t ldy,
+                                    const float* bias, int act, void* workspace,
+                                    size_t workspace_bytes, gcg_stream_t stream) {
+  if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
+  if (gcg_status st = check_dense(Z, ldz, Y, ldy, K, bias, act)) return st;
+  if (plan->n_out > 0 && indptr == nullptr) return fail(GCG_ERR_INVALID_ARG, "indptr is NULL");
+  if (plan->nnz > 0 && (indices == nullptr || vals == nullptr)) return fail(GCG_ERR_INVALID_ARG, "indices/vals NULL");
+  if (K == 0 || plan->n_tasks == 0) return GCG_OK;
+  size_t need = 0;
+  gcg_spmm_plan_workspace_bytes(plan, K, &need);
+  if (need > 0 && (workspace == nullptr || workspace_bytes < need))
+    return fail(GCG_ERR_WORKSPACE, "workspace %zu bytes < %zu needed", workspace_bytes, need);
+  if (need > 0 && !aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "workspace not 16-byte aligned");
+  const int64_t ldws = (K + 3) & ~int64_t{3};
+  float* ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
+               Y, ldy, bias, act, ws, ldws, plan->task_nnz};
+  if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
+  if (plan->n_long > 0) {
+    const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);
+    hipLaunchKernelGGL(spmm_fixup_kernel, grid, dim3(kBlock), 0, st, plan->longs, plan->n_long,
+                       ws, ldws, int(K), Y, ldy, bias, act);
+    GCG_HIP_CHECK(hipGetLastError());
+  }
+  return GCG_OK;
+}
+
+}  // extern "C"
