@@ -216,8 +216,14 @@ class DeviceCSR:
         return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 
 
+def _same_device(t: torch.Tensor, A: "DeviceCSR", name: str):
+    if t.device != A.device:
+        raise ValueError(f"{name} is on {t.device} but the operator lives on {A.device}")
+
+
 def _check_dense(Z: torch.Tensor, A: DeviceCSR):
     _require_cuda(Z, "Z")
+    _same_device(Z, A, "Z")
     if Z.dtype != torch.float32:
         raise TypeError(f"Z must be float32, got {Z.dtype}")
     if Z.dim() != 2 or Z.shape[0] != A.n_cols:
@@ -261,6 +267,7 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         if isinstance(rows, RowSelection):
             sel = rows
         elif isinstance(rows, torch.Tensor) and rows.is_cuda:
+            _same_device(rows, A, "rows")
             rows_dev = rows.to(torch.int32).contiguous()
             mode = "rowwise"
             if rows_dev.numel() and (int(rows_dev.min()) < 0 or int(rows_dev.max()) >= A.n_rows):
@@ -274,6 +281,7 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
     n_out = A.n_rows if rows_dev is None else int(rows_dev.numel())
     if bias is not None:
         _require_cuda(bias, "bias")
+        _same_device(bias, A, "bias")
         if bias.dtype != torch.float32 or bias.numel() != K:
             raise ValueError(f"bias must be float32[{K}]")
         bias = bias.contiguous()
@@ -281,6 +289,7 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         out = empty_dense(n_out, K, A.device)
     else:
         _require_cuda(out, "out")
+        _same_device(out, A, "out")
         if out.shape != (n_out, K) or out.dtype != torch.float32 or (K > 1 and out.stride(1) != 1):
             raise ValueError(f"out must be float32 [{n_out}, {K}] with unit column stride")
     if n_out == 0 or K == 0:
