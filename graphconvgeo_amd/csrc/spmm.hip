@@ -347,7 +347,8 @@ gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
 
 gcg_status check_dense(const float* Z, int64_t ldz, float* Y, int64_t ldy, int64_t K,
                        const float* bias, int act) {
-  if (K < 0 || K > (int64_t{1} << 30)) return fail(GCG_ERR_INVALID_ARG, "bad K=%lld", (long long)K);
+  // grid.y of the fix-up kernel is ceil(K / 64) <= 65535
+  if (K < 0 || K > int64_t{65535} * kWave) return fail(GCG_ERR_INVALID_ARG, "bad K=%lld", (long long)K);
   if (K > 0 && (Z == nullptr || Y == nullptr)) return fail(GCG_ERR_INVALID_ARG, "Z or Y is NULL");
   if (ldz < K || ldy < K) return fail(GCG_ERR_INVALID_ARG, "ldz=%lld / ldy=%lld < K=%lld",
                                       (long long)ldz, (long long)ldy, (long long)K);

@@ -22,7 +22,7 @@
  *
  * Conventions (scipy CSR layout, as `scipy.sparse.csr_matrix` holds it):
  *   indptr  int32[n_rows + 1], indices int32[nnz], vals float32[nnz]; dense operands
- *   are row-major float32 with an explicit leading dimension (elements, >= K).
+ *   are row-major float32 with an explicit leading dimension (elements, >= K), K <= 4,194,240.
  *   All pointers are DEVICE pointers (hipMalloc / torch CUDA tensors) unless the
  *   parameter name ends in `_host`. Nothing in the hot path allocates, synchronizes,
  *   or throws; every function returns a gcg_status (0 = ok). `stream` is a
