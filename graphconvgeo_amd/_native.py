@@ -48,6 +48,8 @@ SIGNATURES = {
                                         C.c_size_t, _psz, _p]),
     "gcg_normalize_adjacency_f32": (C.c_int, [_i64, _i64, _p, _p, C.c_int, _p, _p, _p, _p, _p,
                                               C.c_size_t, _psz, _p, _p]),
+    "gcg_project_mention_graph": (C.c_int, [_i64, _i64, _i64, _p, _p, C.c_int, _p, _p, _i64,
+                                            _pi64, _p, _p]),
     "gcg_spgemm_products": (C.c_int, [_i64, _i64, _p, _p, _i64, _p, _pi64, _p]),
     "gcg_spgemm": (C.c_int, [_i64, _i64, _i64, _i64, _p, _p, _p, C.c_int, _i64, _p, _p, _p,
                              C.c_int, _i64, _p, _p, _p, _p, _p]),

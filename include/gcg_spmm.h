@@ -17,6 +17,7 @@
  *                                               and CSR(X^T) from gcg_csr_transpose_f32
  *   Theano grad of Y[target_indices] (inc_subtensor, duplicates add)
  *                                               gcg_scatter_add_rows_f32
+ *   data.py:226-250,364-370 graph projection    gcg_project_mention_graph
  *   tensormain.py:170-180 H = D^-1/2 (A+I) D^-1/2  gcg_normalize_adjacency_f32
  *   main.py:530 / tensormain.py:114 X_conv = H * X gcg_spgemm_products + gcg_spgemm
  *
@@ -194,6 +195,23 @@ gcg_status gcg_spgemm(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int3
                       const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
                       int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
                       float* c_val, int64_t* nnz_c_dev, gcg_stream_t stream);
+
+/*
+ * Mention-graph projection on the device (DataLoader.get_graph's celebrity filter,
+ * data.py:364-370, then efficient_collaboration_weighted_projected_graph2, data.py:226-250).
+ * Input: the bipartite user/mention graph as incidences (a[e], b[e]) over n_nodes ids, ids <
+ * n_targets are users (their self loops are implicit, as get_graph adds them), ids >= n_targets
+ * mention-only names. A mention node survives iff 1 < degree <= celebrity_threshold. Output:
+ * every pair of users that share a surviving neighbour (a user node's own self loop makes it a
+ * neighbour of itself), deduplicated, u < v, sorted, into caller-owned device arrays out_u /
+ * out_v of `capacity` entries; *n_edges = the edge count. Pass out_u = out_v = NULL to size:
+ * *n_edges then receives the number of pairs before deduplication, an upper bound. Allocates
+ * stream-ordered temporaries and synchronizes `stream`; not a hot-path call.
+ */
+gcg_status gcg_project_mention_graph(int64_t n_targets, int64_t n_nodes, int64_t n_inc,
+                                     const int32_t* a, const int32_t* b, int celebrity_threshold,
+                                     int32_t* out_u, int32_t* out_v, int64_t capacity,
+                                     int64_t* n_edges, int32_t* status_dev, gcg_stream_t stream);
 
 #ifdef __cplusplus
 }

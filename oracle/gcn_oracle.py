@@ -244,3 +244,26 @@ def mlpconv_train(X, H, Y, train_idx, dev_idx, W1, b1, W2, b2, n_epochs, regul_c
             rec["val_acc"] = float((fv["logits"].argmax(axis=1) == yd).mean())
         hist.append(rec)
     return hist, params
+
+
+def project_mentions(n_users, n_nodes, a, b, celebrity_threshold=10):
+    """Pure-Python restatement of get_graph's celebrity filter (data.py:364-370) and
+    efficient_collaboration_weighted_projected_graph2 (data.py:226-250) on the incidence
+    list: users carry self loops; a mention node survives iff 1 < degree <= threshold; every
+    pair of user neighbours of a surviving node becomes an edge. Returns sorted (u < v) pairs."""
+    adj = [set() for _ in range(n_nodes)]
+    for x, y in zip(np.asarray(a).tolist(), np.asarray(b).tolist()):
+        if x != y:
+            adj[x].add(y)
+            adj[y].add(x)
+    dead = {m for m in range(n_users, n_nodes)
+            if len(adj[m]) == 1 or len(adj[m]) > celebrity_threshold}
+    edges = set()
+    for m in range(n_nodes):
+        if m in dead:
+            continue
+        T = sorted({t for t in adj[m] if t < n_users} | ({m} if m < n_users else set()))
+        for i in range(len(T)):
+            for j in range(i + 1, len(T)):
+                edges.add((T[i], T[j]))
+    return np.array(sorted(edges), dtype=np.int64).reshape(-1, 2)
