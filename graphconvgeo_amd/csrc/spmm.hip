@@ -153,8 +153,17 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
-    float* __restrict__ ws, int64_t ldws) {
-  const int w = uniform(static_cast<int>(blockIdx.x) * WPB + (threadIdx.x >> 6));
+    float* __restrict__ ws, int64_t ldws, int xcd_remap) {
+  // Optional XCD-aware mapping (experiment): blocks b and b + 8 share an XCD under the
+  // observed round-robin dispatch, so block b takes task block (b % 8) * ceil(nb / 8) + b / 8
+  // and each XCD walks one contiguous range of rows. Placement is speed-only, never correctness.
+  int blk = static_cast<int>(blockIdx.x);
+  if (xcd_remap) {
+    const int nb = static_cast<int>(gridDim.x), per = (nb + 7) / 8;
+    const int cand = (blk % 8) * per + blk / 8;
+    blk = (nb % 8 == 0) ? cand : blk;  // bijective only when 8 divides the grid
+  }
+  const int w = uniform(blk * WPB + (threadIdx.x >> 6));
   if (w >= n_tasks) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
@@ -261,9 +270,10 @@ struct LaunchArgs {
 template <int VEC, int NCH, int U, int WPB>
 void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   const dim3 grid((a.n_tasks + WPB - 1) / WPB, n_panels);
+  static const int xcd = env_int("GCG_XCD_REMAP");
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
-                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws);
+                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
