@@ -13,9 +13,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 CSRC = os.path.join(PKG_DIR, "csrc")
 # Translation units of libgcg_spmm.so: SpMM kernels + planner, CSR utilities, graph build,
-# SpGEMM, error/version helpers. Compiled in parallel, linked into one shared library.
+# SpGEMM, MFMA dense projection + softmax/xent, error/version helpers. Compiled in parallel, linked into one shared library.
 SOURCES = [os.path.join(CSRC, f) for f in
-           ("spmm.hip", "csr_ops.hip", "graph_build.hip", "spgemm.hip", "errors.cpp")]
+           ("spmm.hip", "csr_ops.hip", "graph_build.hip", "spgemm.hip", "dense.hip", "errors.cpp")]
 INTERNAL_HEADERS = [os.path.join(CSRC, h) for h in ("common.h", "index_kernels.h")]
 HEADER = os.path.join(REPO_DIR, "include", "gcg_spmm.h")
 LIB = os.path.join(PKG_DIR, "libgcg_spmm.so")

@@ -1,0 +1,608 @@
+// dense.hip -- the dense side of the GCN output layer on the CDNA4 matrix cores.
+//
+// Reference (Theano graph, host BLAS):
+//   ConvolutionDenseLayer.get_output_for   T.dot(h, W) + b, softmax     mlpconv.py:86-95
+//   MLPCONV.fit loss                        categorical_crossentropy(    mlpconv.py:229-230
+//                                           softmax(logits), y).mean()
+//   Theano grads of both                    (softmax - onehot)/T, g.W^T, h^T.g
+//
+// Kernels:
+//   gemm_kernel<RT, G, WR, WC, EPI>  C = A.B (+ bias, rectify) with v_mfma_f32_16x16x4_f32
+//       (exact f32 in / f32 accumulate). EPI = 1 fuses the whole output row: bias, softmax,
+//       cross-entropy against int32 labels, first-index argmax, and writes either
+//       (softmax - onehot) * scale (the logits gradient) or the probabilities.
+//   softmax_xent_rows_kernel<NV>     the same row epilogue for logits that already exist
+//       (the reference order, where the logits come out of the H SpMM, mlpconv.py:90-94).
+//
+// Work decomposition (64-wide waves, 4 per workgroup, WR x WC of them):
+//   workgroup tile  BM = 16*RT*WR rows  x  BN = 64*G*WC columns
+//   wave tile       16*RT rows x 64*G columns = RT x (4G) MFMA 16x16 tiles
+// A (rows x K) is staged through LDS in KC-deep chunks (double-buffered through registers),
+// shared by the WC waves of a row band. B (K x N, row-major, e.g. W: 1.1 MB at K=300,
+// C=930, L2-resident) is read straight into VGPRs: lane (j = l&15, q = l>>4) loads ONE
+// dwordx4 B[k][c0 + 4j .. 4j+3] per k-step and uses its 4 floats as the B fragment of 4
+// different 16-column tiles (tile e covers columns c0 + 4j + e). The accumulator registers
+// then hold 4 adjacent columns per lane for every row -> dwordx4 stores, no shuffles.
+// The k order inside a 16-deep step is permuted consistently for A and B (step e uses
+// k = k0 + 4q + e), so each lane reads A as one dwordx4 from LDS as well.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <limits>
+
+#include "common.h"
+
+using namespace gcg;
+
+namespace {
+
+using f4 = __attribute__((ext_vector_type(4))) float;
+
+__device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+}
+
+template <int W>
+__device__ __forceinline__ float reduce16_max(float v) {
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+template <int W>
+__device__ __forceinline__ float reduce16_sum(float v) {
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+template <int W>
+__device__ __forceinline__ int reduce16_min(int v) {
+#pragma unroll
+  for (int o = 1; o < W; o <<= 1) v = min(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+constexpr float kNegInf = -std::numeric_limits<float>::infinity();
+
+template <int RT, int G, int WR, int WC, int EPI>
+__global__ __launch_bounds__(256, 1) void gemm_kernel(
+    int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+    int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
+    const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows) {
+  static_assert(WR * WC == 4, "4 waves per workgroup");
+  constexpr int BM = 16 * RT * WR;
+  constexpr int BN = 64 * G * WC;
+  constexpr int KC = 32;                   // k depth of one LDS chunk
+  constexpr int KP = KC + 4;               // padded LDS row (floats)
+  constexpr int A4 = BM * KC / 4 / 256;    // A dwordx4 per thread per chunk
+  static_assert(A4 >= 1 && BM * KC / 4 % 256 == 0, "A chunk must split evenly");
+  __shared__ float As[2][BM][KP];
+  __shared__ float red[3][WC][BM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // scalar: uniform branches
+  const int wr = wave / WC, wc = wave % WC;
+  const int j = lane & 15, q = lane >> 4;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int colw = blockIdx.y * BN + wc * G * 64;  // this wave's first column
+  const int n4 = (N + 3) & ~3;                     // columns B may be read at (<= ldb)
+
+  // Per-lane B column offsets (clamped in range; out-of-range columns are never stored).
+  int bcol[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int c = colw + 64 * g + 4 * j;
+    bcol[g] = c < n4 ? c : 0;
+  }
+  const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
+
+  f4 acc[RT][G][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- A staging: chunk c covers k in [c*KC, c*KC + KC) ----
+  // Branch-free: row and column are clamped into the operand and out-of-range elements are
+  // zeroed by selects, so the loop body is straight-line and hipcc keeps counted vmcnt waits
+  // (a branchy load makes it drain every load in flight). A 16-B load at a clamped column
+  // stays inside the 16-B aligned block of a valid element, hence inside the allocation.
+  const int kmax4 = (K - 1) & ~3;  // last 4-aligned column start with a valid element
+  f4 areg[A4];
+  auto load_a = [&](int kc0) {
+#pragma unroll
+    for (int i = 0; i < A4; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx / (KC / 4), k = kc0 + (idx % (KC / 4)) * 4;
+      const int64_t gr = row0 + r;
+      const int64_t rr = gr < M ? gr : M - 1;
+      const int kk = k < kmax4 ? k : kmax4;
+      f4 v = *reinterpret_cast<const f4*>(A + rr * lda + kk);
+      const bool rowok = gr < M;
+      v.x = (rowok && k < K) ? v.x : 0.f;
+      v.y = (rowok && k + 1 < K) ? v.y : 0.f;
+      v.z = (rowok && k + 2 < K) ? v.z : 0.f;
+      v.w = (rowok && k + 3 < K) ? v.w : 0.f;
+      areg[i] = v;
+    }
+  };
+  auto store_a = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < A4; ++i) {
+      const int idx = tid + 256 * i;
+      const int r = idx / (KC / 4), k4 = (idx % (KC / 4)) * 4;
+      *reinterpret_cast<f4*>(&As[buf][r][k4]) = areg[i];
+    }
+  };
+  // Workgroup barrier for the LDS hand-off only: waits for this wave's LDS traffic, not for
+  // its global loads (a __syncthreads() fence would drain the B prefetch every chunk).
+  auto lds_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  // ---- B fragments for one 16-deep k-step: bf[g][e] = B[k0 + 4q + e][bcol[g] .. +3] ----
+  auto load_b = [&](f4 (&bf)[G][4], int k0) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      int k = k0 + 4 * q + e;
+      k = k < K ? k : K - 1;  // A is zero there; any finite B row does
+      const float* brow = B + static_cast<int64_t>(k) * ldb;
+#pragma unroll
+      for (int g = 0; g < G; ++g) bf[g][e] = *reinterpret_cast<const f4*>(brow + bcol[g]);
+    }
+  };
+
+  const int arow = wr * 16 * RT + j;
+  auto compute = [&](const f4 (&bf)[G][4], int buf, int s) {
+    f4 af[RT];
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+      af[t] = *reinterpret_cast<const f4*>(&As[buf][arow + 16 * t][s * 16 + 4 * q]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        if (g >= ngv) continue;  // scalar branch: group entirely past N
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          acc[t][g][0] = mfma4(af[t][e], bf[g][e].x, acc[t][g][0]);
+          acc[t][g][1] = mfma4(af[t][e], bf[g][e].y, acc[t][g][1]);
+          acc[t][g][2] = mfma4(af[t][e], bf[g][e].z, acc[t][g][2]);
+          acc[t][g][3] = mfma4(af[t][e], bf[g][e].w, acc[t][g][3]);
+        }
+      }
+  };
+
+  // Main loop, one 32-deep chunk (two 16-deep steps) per iteration, straight-line: B
+  // ping-pongs between two register sets (step 2c in b0, 2c+1 in b1, each loaded one step
+  // ahead), A chunk c+1 is loaded to registers during chunk c and written to the other LDS
+  // buffer after it.
+  static_assert(KC == 32, "two 16-deep steps per chunk");
+  const int n_chunks = (K + KC - 1) / KC;
+  load_a(0);
+  store_a(0);
+  lds_barrier();
+  f4 b0[G][4], b1[G][4];
+  load_b(b0, 0);
+  for (int c = 0; c < n_chunks; ++c) {
+    const int buf = c & 1;
+    const int k0 = c * KC;
+    load_a(k0 + KC);  // past K: clamped and zeroed, never used
+    load_b(b1, k0 + 16);
+    compute(b0, buf, 0);
+    load_b(b0, k0 + 32);
+    if (k0 + 16 < K) compute(b1, buf, 1);
+    store_a(buf ^ 1);
+    lds_barrier();
+  }
+
+  // ---- epilogue ----
+  // lane holds, for row  row0 + wr*16*RT + 16t + 4q + r  and column  colw + 64g + 4j + e,
+  // the value acc[t][g][e][r].
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bv[g] = f4{0.f, 0.f, 0.f, 0.f};
+    const int c = colw + 64 * g + 4 * j;
+    if (bias != nullptr) {
+      if (c < N) bv[g].x = bias[c];
+      if (c + 1 < N) bv[g].y = bias[c + 1];
+      if (c + 2 < N) bv[g].z = bias[c + 2];
+      if (c + 3 < N) bv[g].w = bias[c + 3];
+    }
+  }
+
+  if constexpr (EPI == 0) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + wr * 16 * RT + 16 * t + 4 * q + r;
+        if (row >= M) continue;
+        float* crow = Cout + row * ldc;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int c = colw + 64 * g + 4 * j;
+          if (c >= N) continue;
+          f4 v = {acc[t][g][0][r] + bv[g].x, acc[t][g][1][r] + bv[g].y,
+                  acc[t][g][2][r] + bv[g].z, acc[t][g][3][r] + bv[g].w};
+          if (act == GCG_ACT_RELU) {  // Theano rectify 0.5*(x+|x|), mlpconv.py:77
+            v.x = 0.5f * (v.x + fabsf(v.x)); v.y = 0.5f * (v.y + fabsf(v.y));
+            v.z = 0.5f * (v.z + fabsf(v.z)); v.w = 0.5f * (v.w + fabsf(v.w));
+          }
+          if (c + 3 < N) {
+            *reinterpret_cast<f4*>(crow + c) = v;
+          } else {
+            crow[c] = v.x;
+            if (c + 1 < N) crow[c + 1] = v.y;
+            if (c + 2 < N) crow[c + 2] = v.z;
+          }
+        }
+      }
+  } else {
+    // Whole row in this workgroup (host guarantees BN >= N, gridDim.y == 1). One 16-row
+    // MFMA tile at a time (4 rows per lane live), partial row results combined over the
+    // WC waves of the row band through LDS.
+    if (scale_dev != nullptr) scale *= *scale_dev;
+    const int rb = wr * 16 * RT;  // first row of this wave's band inside the block
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      float mx[4], sm[4], xy[4];
+      int am[4], yl[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + rb + 16 * t + 4 * q + r;
+        yl[r] = (labels != nullptr && row < M) ? labels[row] : -1;
+      }
+      // 1) bias, mask, row max
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float m = kNegInf;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = colw + 64 * g + 4 * j + e;
+            float v = acc[t][g][e][r] + bv[g][e];
+            v = c < N ? v : kNegInf;
+            acc[t][g][e][r] = v;
+            m = fmaxf(m, v);
+          }
+        mx[r] = reduce16_max<16>(m);
+      }
+      if (j == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) red[0][wc][rb + 16 * t + 4 * q + r] = mx[r];
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = rb + 16 * t + 4 * q + r;
+        float m = red[0][0][rr];
+#pragma unroll
+        for (int w = 1; w < WC; ++w) m = fmaxf(m, red[0][w][rr]);
+        mx[r] = m;
+      }
+      __syncthreads();
+      // 2) sum of exp, logit of the label, first index of the max
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float sv = 0.f, x = 0.f;
+        int a = 0x7fffffff;
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int c = colw + 64 * g + 4 * j + e;
+            const float v = acc[t][g][e][r];
+            sv += expf(v - mx[r]);  // exp(-inf) = 0 for masked columns
+            x += (c == yl[r]) ? v : 0.f;
+            a = (v == mx[r] && c < a) ? c : a;
+          }
+        sm[r] = reduce16_sum<16>(sv);
+        xy[r] = reduce16_sum<16>(x);
+        am[r] = reduce16_min<16>(a);
+      }
+      if (j == 0) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int rr = rb + 16 * t + 4 * q + r;
+          red[0][wc][rr] = sm[r];
+          red[1][wc][rr] = xy[r];
+          red[2][wc][rr] = __int_as_float(am[r]);
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int rr = rb + 16 * t + 4 * q + r;
+        float sv = red[0][0][rr], x = red[1][0][rr];
+        int a = __float_as_int(red[2][0][rr]);
+#pragma unroll
+        for (int w = 1; w < WC; ++w) {
+          sv += red[0][w][rr];
+          x += red[1][w][rr];
+          a = min(a, __float_as_int(red[2][w][rr]));
+        }
+        sm[r] = sv;
+        xy[r] = x;
+        am[r] = a;
+      }
+      __syncthreads();  // red is reused by the next tile
+      // 3) outputs
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int64_t row = row0 + rb + 16 * t + 4 * q + r;
+        if (row >= M) continue;
+        const float inv = 1.0f / sm[r];
+        const bool xent = yl[r] >= 0;
+        if (xent && wc == 0 && j == 0) {
+          loss_rows[row] = (mx[r] + logf(sm[r])) - xy[r];  // -log softmax[row, y]
+          if (correct_rows) correct_rows[row] = (am[r] == yl[r]) ? 1.f : 0.f;
+        }
+        if (Cout == nullptr) continue;  // loss / accuracy only (evaluation)
+        float* orow = Cout + row * ldc;
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+          const int c = colw + 64 * g + 4 * j;
+          if (c >= N) continue;
+          f4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            float p = expf(acc[t][g][e][r] - mx[r]) * inv;
+            if (xent) p = (p - ((c + e) == yl[r] ? 1.f : 0.f)) * scale;
+            o[e] = p;
+          }
+          if (c + 3 < N) {
+            *reinterpret_cast<f4*>(orow + c) = o;
+          } else {
+            orow[c] = o.x;
+            if (c + 1 < N) orow[c + 1] = o.y;
+            if (c + 2 < N) orow[c + 2] = o.z;
+          }
+        }
+      }
+    }
+  }
+}
+
+// One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
+// exp, label logit and first-index argmax, then dlogits / probabilities. In-place safe.
+template <int NV>
+__global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
+    int M, int N, const float* __restrict__ L, int64_t ldl, const int32_t* __restrict__ labels,
+    float scale, const float* __restrict__ scale_dev, float* O, int64_t ldo,
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows, int vec) {
+  const int lane = threadIdx.x & 63;
+  const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* lrow = L + row * ldl;
+  f4 v[NV];
+  float m = kNegInf;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    if (vec && c + 3 < N) {
+      v[i] = *reinterpret_cast<const f4*>(lrow + c);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[i][e] = (c + e < N) ? lrow[c + e] : kNegInf;
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) m = fmaxf(m, v[i][e]);
+  }
+  m = reduce16_max<64>(m);
+  const int y = labels ? labels[row] : -1;
+  float s = 0.f, x = 0.f;
+  int a = 0x7fffffff;
+#pragma unroll
+  for (int i = 0; i < NV; ++i)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = 4 * (lane + 64 * i) + e;
+      s += expf(v[i][e] - m);
+      x += (c == y) ? v[i][e] : 0.f;
+      a = (v[i][e] == m && c < a) ? c : a;
+    }
+  s = reduce16_sum<64>(s);
+  x = reduce16_sum<64>(x);
+  a = reduce16_min<64>(a);
+  if (y >= 0 && lane == 0) {
+    loss_rows[row] = (m + logf(s)) - x;
+    if (correct_rows) correct_rows[row] = (a == y) ? 1.f : 0.f;
+  }
+  if (O == nullptr) return;  // loss / accuracy only
+  if (scale_dev != nullptr) scale *= *scale_dev;
+  const float inv = 1.0f / s;
+  float* orow = O + row * ldo;
+#pragma unroll
+  for (int i = 0; i < NV; ++i) {
+    const int c = 4 * (lane + 64 * i);
+    if (c >= N) continue;
+    f4 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float p = expf(v[i][e] - m) * inv;
+      if (y >= 0) p = (p - ((c + e) == y ? 1.f : 0.f)) * scale;
+      o[e] = p;
+    }
+    if (vec && c + 3 < N) {
+      *reinterpret_cast<f4*>(orow + c) = o;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (c + e < N) orow[c + e] = o[e];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------------------
+
+struct Shape {
+  int RT, G, WR, WC;
+  int bm() const { return 16 * RT * WR; }
+  int bn() const { return 64 * G * WC; }
+};
+
+// Instantiated tiles. Row-band (WC = 4) tiles keep a whole output row of up to 1024
+// columns in one workgroup (needed by the fused softmax); WR = 4 tiles serve narrow N.
+template <int EPI>
+gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, int K,
+                       const float* A, int64_t lda, const float* B, int64_t ldb,
+                       const float* bias, int act, float* C, int64_t ldc, const int32_t* labels,
+                       float scale, const float* scale_dev, float* loss_rows,
+                       float* correct_rows) {
+#define GCG_GEMM_CASE(rt, g, wr, wc)                                                        \
+  if (s.RT == rt && s.G == g && s.WR == wr && s.WC == wc) {                                  \
+    hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI>), grid, dim3(256), 0, st, M, N, K, A, \
+                       lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
+                       correct_rows);                                                         \
+    GCG_HIP_CHECK(hipGetLastError());                                                         \
+    return GCG_OK;                                                                            \
+  }
+  GCG_GEMM_CASE(2, 1, 1, 4)
+  GCG_GEMM_CASE(2, 2, 1, 4)
+  GCG_GEMM_CASE(2, 3, 1, 4)
+  GCG_GEMM_CASE(2, 4, 1, 4)
+  GCG_GEMM_CASE(4, 4, 1, 4)
+  GCG_GEMM_CASE(4, 2, 1, 4)
+  GCG_GEMM_CASE(4, 3, 1, 4)
+  GCG_GEMM_CASE(2, 1, 4, 1)
+  GCG_GEMM_CASE(2, 2, 4, 1)
+  GCG_GEMM_CASE(2, 3, 4, 1)
+  GCG_GEMM_CASE(2, 4, 4, 1)
+  GCG_GEMM_CASE(2, 5, 4, 1)
+#undef GCG_GEMM_CASE
+  return fail(GCG_ERR_INVALID_ARG, "gemm: no tile instantiated for RT=%d G=%d WR=%d WC=%d", s.RT,
+              s.G, s.WR, s.WC);
+}
+
+// Tile choice. fused: the workgroup must hold the whole row (WC = 4, G = ceil(N/256)).
+// Plain: narrow N (<= 320) -> one wave spans all columns and 4 waves split 128 rows;
+// wider N -> row bands of 32 rows x up to 1024 columns, grid.y for the rest.
+Shape pick_shape(int64_t N, bool fused) {
+  const int groups = static_cast<int>((N + 63) / 64);
+  // Row tiles per wave of the wide (WC = 4) tiles: 4 (64-row workgroups) halves the L2 traffic
+  // of B per flop; measured 92.6 vs 83.2 TFLOP/s (plain) and 78.6 vs 72.3 (fused) on
+  // Twitter-World's 840k x 300 x 930. GCG_GEMM_RT=2 selects the smaller tile (experiments).
+  const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
+  if (fused || groups > 5) {
+    const int g = std::min(4, (groups + 3) / 4);
+    return Shape{g >= 2 ? rt : 2, std::max(g, 1), 1, 4};
+  }
+  return Shape{2, std::max(groups, 1), 4, 1};
+}
+
+gcg_status check_dense(const char* fn, const float* p, int64_t ld, int64_t cols, bool vec4) {
+  if (p == nullptr) return fail(GCG_ERR_INVALID_ARG, "%s: null operand", fn);
+  if (ld < cols) return fail(GCG_ERR_INVALID_ARG, "%s: leading dimension %lld < %lld", fn,
+                             static_cast<long long>(ld), static_cast<long long>(cols));
+  if (vec4 && (ld % 4 != 0 || !aligned(p, 16)))
+    return fail(GCG_ERR_MISALIGNED, "%s: operand needs a 16-B aligned base and ld %% 4 == 0", fn);
+  if (!aligned(p, 4)) return fail(GCG_ERR_MISALIGNED, "%s: operand not 4-B aligned", fn);
+  return GCG_OK;
+}
+
+gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t K,
+                       const float* A, int64_t lda, const float* B, int64_t ldb,
+                       const float* bias, int act, float* C, int64_t ldc,
+                       const int32_t* labels, float scale, const float* scale_dev,
+                       float* loss_rows, float* correct_rows, gcg_stream_t stream) {
+  if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
+                static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
+  if (fused && N > 1024)
+    return fail(GCG_ERR_INVALID_ARG, "%s: N=%lld > 1024 columns per fused row", fn,
+                static_cast<long long>(N));
+  if (act != GCG_ACT_NONE && act != GCG_ACT_RELU)
+    return fail(GCG_ERR_INVALID_ARG, "%s: unknown act %d", fn, act);
+  gcg_status s;
+  if ((s = check_dense(fn, A, lda, K, true)) != GCG_OK) return s;
+  // B is read as dwordx4 at columns < round4(N): its row stride must cover them.
+  if ((s = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
+  if (!(fused && C == nullptr && labels != nullptr) &&
+      (s = check_dense(fn, C, ldc, N, true)) != GCG_OK)
+    return s;
+  if (labels != nullptr && loss_rows == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "%s: labels given without loss_rows", fn);
+  if (M == 0) return GCG_OK;
+  const Shape sh = pick_shape(N, fused);
+  dim3 grid(static_cast<unsigned>((M + sh.bm() - 1) / sh.bm()),
+            static_cast<unsigned>((N + sh.bn() - 1) / sh.bn()));
+  if (grid.x > 0x7fffffffu) return fail(GCG_ERR_INVALID_ARG, "%s: M too large", fn);
+  auto st = static_cast<hipStream_t>(stream);
+  if (fused)
+    return launch_gemm<1>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
+                          labels, scale, scale_dev, loss_rows, correct_rows);
+  return launch_gemm<0>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
+                        nullptr, 0.f, nullptr, nullptr, nullptr);
+}
+
+}  // namespace
+
+extern "C" {
+
+gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                        const float* B, int64_t ldb, const float* bias, int act, float* C,
+                        int64_t ldc, gcg_stream_t stream) {
+  return gemm_common("gcg_gemm_f32", false, M, N, K, A, lda, B, ldb, bias, act, C, ldc, nullptr,
+                     0.f, nullptr, nullptr, nullptr, stream);
+}
+
+gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
+                                        int64_t lda, const float* W, int64_t ldw,
+                                        const float* bias, const int32_t* labels, float scale,
+                                        const float* scale_dev, float* out, int64_t ldo,
+                                        float* loss_rows, float* correct_rows,
+                                        gcg_stream_t stream) {
+  return gemm_common("gcg_project_softmax_xent_f32", true, M, N, K, A, lda, W, ldw, bias,
+                     GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows, correct_rows,
+                     stream);
+}
+
+gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
+                                const int32_t* labels, float scale, const float* scale_dev,
+                                float* out, int64_t ldo, float* loss_rows, float* correct_rows,
+                                gcg_stream_t stream) {
+  const char* fn = "gcg_softmax_xent_f32";
+  if (M < 0 || N <= 0 || M > INT32_MAX || N > 4096)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld (N <= 4096)", fn,
+                static_cast<long long>(M), static_cast<long long>(N));
+  gcg_status s;
+  if ((s = check_dense(fn, logits, ldl, N, false)) != GCG_OK) return s;
+  if (out != nullptr && (s = check_dense(fn, out, ldo, N, false)) != GCG_OK) return s;
+  if (labels != nullptr && loss_rows == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "%s: labels given without loss_rows", fn);
+  if (out == nullptr && labels == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "%s: nothing to compute (no out, no labels)", fn);
+  if (M == 0) return GCG_OK;
+  const int vec = (ldl % 4 == 0 && aligned(logits, 16) &&
+                   (out == nullptr || (ldo % 4 == 0 && aligned(out, 16)))) ? 1 : 0;
+  const int nv = static_cast<int>((N + 255) / 256);
+  dim3 grid(static_cast<unsigned>((M + 3) / 4));
+  auto st = static_cast<hipStream_t>(stream);
+#define GCG_SX_CASE(v)                                                                       \
+  if (nv <= v) {                                                                             \
+    hipLaunchKernelGGL(softmax_xent_rows_kernel<v>, grid, dim3(256), 0, st, int(M), int(N), \
+                       logits, ldl, labels, scale, scale_dev, out, ldo, loss_rows,          \
+                       correct_rows, vec);                                                   \
+    GCG_HIP_CHECK(hipGetLastError());                                                        \
+    return GCG_OK;                                                                           \
+  }
+  GCG_SX_CASE(1)
+  GCG_SX_CASE(2)
+  GCG_SX_CASE(4)
+  GCG_SX_CASE(8)
+  GCG_SX_CASE(16)
+#undef GCG_SX_CASE
+  return fail(GCG_ERR_INVALID_ARG, "%s: N too large", fn);
+}
+
+}  // extern "C"

@@ -1,0 +1,289 @@
+"""Dense side of the output layer on the MI355X matrix cores (host mirror of T.dot + softmax +
+categorical_crossentropy).
+
+Reference (Theano, host BLAS / CPU):
+    ConvolutionDenseLayer.get_output_for   T.dot(h, W), (... + b), softmax   mlpconv.py:86-95
+    MLPCONV loss / accuracy                categorical_crossentropy(out, y).mean(),
+                                           T.mean(T.eq(out.argmax(-1), y))    mlpconv.py:227-253
+    predict_proba                          softmax rows                       mlpconv.py:329-335
+
+Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
+  matmul(A, W)                    C = A . W          gcg_gemm_f32 (grad A: g . W^T, same kernel)
+  project_softmax_xent(P, W, b, y)  loss, acc of softmax(P . W + b) against y, one fused
+                                  kernel that never writes the logits; its gradient
+                                  (softmax - onehot)/T is produced in the same pass
+  softmax_xent(logits, y)         loss, acc of logits that already exist (reference order)
+  softmax(logits)                 predict_proba
+The weight-gradient reduction over rows (h^T . g, K x C) stays a library GEMM (torch.matmul
+-> hipBLASLt): it is a plain tall-skinny GEMM with nothing to fuse.
+There is no CPU path: CPU tensors raise.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call
+from .sparse import _ptr, _require_cuda, _stream_handle, empty_dense
+
+FUSED_MAX_COLS = 1024
+ROWS_MAX_COLS = 4096
+
+
+def _ld(t: torch.Tensor) -> int:
+    """Row stride in elements; a single row's stride is never used, so report round4(cols)."""
+    return t.stride(0) if t.shape[0] > 1 else (max(t.shape[1], 1) + 3) // 4 * 4
+
+
+def _aligned_operand(t: torch.Tensor, name: str) -> torch.Tensor:
+    """A row-major fp32 operand with a 16-B aligned base and ld % 4 == 0 (copied if not)."""
+    _require_cuda(t, name)
+    if t.dtype != torch.float32 or t.dim() != 2:
+        raise TypeError(f"{name} must be a 2-D float32 tensor")
+    ok = (t.shape[1] <= 1 or t.stride(1) == 1) and _ld(t) % 4 == 0 and t.data_ptr() % 16 == 0
+    if ok:
+        return t
+    out = empty_dense(t.shape[0], t.shape[1], t.device)
+    out.copy_(t)
+    return out
+
+
+class _WeightCache:
+    """Padded [K, round4(N)] (or transposed [N, round4(K)]) copy of a weight, rebuilt only
+    when the parameter changes (its in-place version counter moves, e.g. after Adam)."""
+
+    def __init__(self):
+        self._key = None
+        self._buf = None
+
+    def get(self, W: torch.Tensor, transpose: bool, scale: Optional[torch.Tensor] = None):
+        key = (W.data_ptr(), W._version, tuple(W.shape), transpose)
+        capturing = torch.cuda.is_current_stream_capturing()
+        if scale is None and key == self._key and not capturing:
+            return self._buf  # a captured graph always re-copies: W moves between replays
+        src = W.detach().t() if transpose else W.detach()
+        rows, cols = src.shape
+        if self._buf is None or self._buf.shape != (rows, cols) or self._buf.device != W.device:
+            ldp = (cols + 3) // 4 * 4
+            full = torch.zeros((rows, ldp), dtype=torch.float32, device=W.device)
+            self._buf = full[:, :cols]
+        if scale is not None:
+            torch.mul(src, scale, out=self._buf)
+            self._key = None
+        else:
+            self._buf.copy_(src)
+            self._key = key
+        return self._buf
+
+
+def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
+         act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = act(A . B + bias) on the MFMA kernel. B must have ld >= round4(N) (see
+    _WeightCache); A is copied to an aligned buffer if its rows are not 16-B aligned."""
+    A = _aligned_operand(A, "A")
+    _require_cuda(B, "B")
+    M, K = A.shape
+    if B.dim() != 2 or B.shape[0] != K:
+        raise ValueError(f"shape mismatch: A is {tuple(A.shape)}, B is {tuple(B.shape)}")
+    N = B.shape[1]
+    if B.dtype != torch.float32 or (N > 1 and B.stride(1) != 1):
+        raise TypeError("B must be float32 with unit column stride")
+    ldb = B.stride(0)
+    if ldb < (N + 3) // 4 * 4 or ldb % 4 or B.data_ptr() % 16:
+        raise ValueError("B needs ld >= round4(N), ld % 4 == 0 and a 16-B aligned base")
+    if bias is not None:
+        _require_cuda(bias, "bias")
+        if bias.numel() != N or bias.dtype != torch.float32:
+            raise ValueError(f"bias must be float32[{N}]")
+        bias = bias.contiguous()
+    if out is None:
+        out = empty_dense(M, N, A.device)
+    elif out.shape != (M, N) or out.dtype != torch.float32 or (N > 1 and out.stride(1) != 1):
+        raise ValueError(f"out must be float32 [{M}, {N}] with unit column stride")
+    if M == 0:
+        return out
+    actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
+    with torch.cuda.device(A.device):
+        call("gcg_gemm_f32", M, N, K, _ptr(A), _ld(A), _ptr(B), ldb, _ptr(bias), actc,
+             _ptr(out), _ld(out), _stream_handle(A.device))
+    return out
+
+
+class _MatMul(torch.autograd.Function):
+    """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88); dA = g . W^T on the MFMA kernel,
+    dW = A^T . g, db = colsum(g)."""
+
+    @staticmethod
+    def forward(ctx, A, W, b, cache_fwd: _WeightCache, cache_bwd: _WeightCache):
+        C = gemm(A, cache_fwd.get(W, transpose=False), bias=None if b is None else b.detach())
+        ctx.save_for_backward(A, W)
+        ctx.cache_bwd = cache_bwd
+        ctx.has_b = b is not None
+        return C
+
+    @staticmethod
+    def backward(ctx, g):
+        A, W = ctx.saved_tensors
+        gA = gW = gb = None
+        if ctx.needs_input_grad[0]:
+            gA = gemm(g, ctx.cache_bwd.get(W, transpose=True))
+        if ctx.needs_input_grad[1]:
+            gW = torch.matmul(A.t(), g)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = g.sum(dim=0)
+        return gA, gW, gb, None, None
+
+
+class Projection:
+    """Holds the padded weight copies of one dense weight W (K x C) for the MFMA kernels."""
+
+    def __init__(self):
+        self.fwd = _WeightCache()
+        self.bwd = _WeightCache()
+
+    def matmul(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None
+               ) -> torch.Tensor:
+        return _MatMul.apply(A, W, b, self.fwd, self.bwd)
+
+    def softmax_xent(self, P, W, b, labels):
+        return _ProjectXent.apply(P, W, b, labels, self)
+
+    def probabilities(self, P, W, b) -> torch.Tensor:
+        """softmax(P . W + b) rows (predict_proba) in one fused launch."""
+        P = _aligned_operand(P, "P")
+        M = P.shape[0]
+        out = empty_dense(M, W.shape[1], P.device)
+        _fused(P, self.fwd.get(W, False), b, None, 1.0, None, out, None, None)
+        return out
+
+
+def _labels_i32(labels: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    _require_cuda(labels, "labels")
+    if labels.numel() != M:
+        raise ValueError(f"labels has {labels.numel()} entries for {M} rows")
+    return labels.to(torch.int32).contiguous()
+
+
+def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct):
+    P = _aligned_operand(P, "P")
+    M, K = P.shape
+    N = Wp.shape[1]
+    if Wp.shape[0] != K:
+        raise ValueError(f"shape mismatch: P is {tuple(P.shape)}, W is {tuple(Wp.shape)}")
+    if N > FUSED_MAX_COLS:
+        raise ValueError(f"fused softmax projection supports up to {FUSED_MAX_COLS} classes")
+    if b is not None:
+        _require_cuda(b, "b")
+        b = b.detach().contiguous()
+    if M == 0:
+        return
+    with torch.cuda.device(P.device):
+        call("gcg_project_softmax_xent_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp), Wp.stride(0),
+             _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
+             _ld(out) if out is not None else 0, _ptr(loss_rows), _ptr(correct),
+             _stream_handle(P.device))
+
+
+class _ProjectXent(torch.autograd.Function):
+    """(loss, acc) = mean CE / accuracy of softmax(P . W + b) against labels.
+
+    Forward: one fused MFMA launch writes G = (softmax - onehot)/M (the logits gradient),
+    per-row losses and hits; no logits in HBM. Backward (upstream g): dP = G . (g W)^T
+    (MFMA kernel, g folded into the small transposed weight copy), dW = g P^T . G,
+    db = g colsum(G)."""
+
+    @staticmethod
+    def forward(ctx, P, W, b, labels, proj: Projection):
+        P = _aligned_operand(P, "P")
+        M, N = P.shape[0], W.shape[1]
+        y = _labels_i32(labels, M, N)
+        need_grad = any(ctx.needs_input_grad[:3])
+        G = empty_dense(M, N, P.device) if need_grad else None
+        loss_rows = torch.empty(M, dtype=torch.float32, device=P.device)
+        correct = torch.empty(M, dtype=torch.float32, device=P.device)
+        _fused(P, proj.fwd.get(W, False), b, y, 1.0 / max(M, 1), None, G, loss_rows, correct)
+        ctx.save_for_backward(P, W, G)
+        ctx.proj = proj
+        ctx.has_b = b is not None
+        loss = loss_rows.mean()
+        acc = correct.mean()
+        ctx.mark_non_differentiable(acc)
+        return loss, acc
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_acc):
+        P, W, G = ctx.saved_tensors
+        gP = gW = gb = None
+        g = g_loss.reshape(())
+        if ctx.needs_input_grad[0]:
+            gP = gemm(G, ctx.proj.bwd.get(W, transpose=True, scale=g))
+        if ctx.needs_input_grad[1]:
+            gW = torch.matmul(P.t(), G).mul_(g)
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = G.sum(dim=0).mul_(g)
+        return gP, gW, gb, None, None
+
+
+def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct):
+    M, N = logits.shape
+    if N > ROWS_MAX_COLS:
+        raise ValueError(f"softmax_xent supports up to {ROWS_MAX_COLS} classes")
+    if M == 0:
+        return
+    with torch.cuda.device(logits.device):
+        call("gcg_softmax_xent_f32", M, N, _ptr(logits), _ld(logits), _ptr(y), float(scale),
+             _ptr(scale_dev), _ptr(out), _ld(out) if out is not None else 0, _ptr(loss_rows),
+             _ptr(correct), _stream_handle(logits.device))
+
+
+class _SoftmaxXent(torch.autograd.Function):
+    """(loss, acc) of logits that exist (the reference order: logits = (H . Z2 + b)[idx]).
+    Forward reads the logits once (loss and hits only); backward writes
+    g (softmax - onehot)/M in one more pass, g read on the device (graph-capturable)."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        _require_cuda(logits, "logits")
+        if logits.dtype != torch.float32 or logits.dim() != 2 or \
+                (logits.shape[1] > 1 and logits.stride(1) != 1):
+            raise TypeError("logits must be 2-D float32 with unit column stride")
+        M, N = logits.shape
+        y = _labels_i32(labels, M, N)
+        loss_rows = torch.empty(M, dtype=torch.float32, device=logits.device)
+        correct = torch.empty(M, dtype=torch.float32, device=logits.device)
+        _rows_call(logits, y, 1.0, None, None, loss_rows, correct)
+        ctx.save_for_backward(logits, y)
+        acc = correct.mean()
+        ctx.mark_non_differentiable(acc)
+        return loss_rows.mean(), acc
+
+    @staticmethod
+    def backward(ctx, g_loss, _g_acc):
+        logits, y = ctx.saved_tensors
+        M, N = logits.shape
+        gl = empty_dense(M, N, logits.device)
+        dummy = torch.empty(M, dtype=torch.float32, device=logits.device)
+        g = g_loss.reshape(1).to(torch.float32).contiguous()
+        _rows_call(logits, y, 1.0 / max(M, 1), g, gl, dummy, None)
+        return gl, None
+
+
+def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None
+                         ) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mean CE loss, accuracy) of softmax(P . W + b) against labels, differentiable in P, W, b."""
+    return _ProjectXent.apply(P, W, b, labels, proj or Projection())
+
+
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mean CE loss, accuracy) of existing logits, differentiable in the logits."""
+    return _SoftmaxXent.apply(logits, labels)
+
+
+def softmax(logits: torch.Tensor) -> torch.Tensor:
+    """Row softmax (predict_proba) through the row kernel."""
+    _require_cuda(logits, "logits")
+    M, N = logits.shape
+    out = empty_dense(M, N, logits.device)
+    _rows_call(logits, None, 1.0, None, out, None, None)
+    return out

@@ -234,14 +234,18 @@ class ConvolutionDenseLayer(GraphConvLayer):
             order = "propagate_first" if self.num_units > self.num_inputs else "reference"
         self.order = order
 
-    def forward(self, input, target_indices=None, **kwargs):
-        if self.order == "reference" or isinstance(input, gs.DeviceCSR) or sps.issparse(input):
-            return super().forward(input, target_indices=target_indices, **kwargs)
+    def propagate(self, input, target_indices=None) -> torch.Tensor:
+        """(H . h)[target_indices] -- the K-wide SpMM of the propagate-first order."""
         rows = None
         if target_indices is not None:
             rows = target_indices if isinstance(target_indices, gs.RowSelection) else \
                 gs.RowSelection(target_indices, self.device)
-        P = csr_matmul(self.H, input, None, None, rows, self.mode)  # (H . h)[rows], K wide
+        return csr_matmul(self.H, input, None, None, rows, self.mode)
+
+    def forward(self, input, target_indices=None, **kwargs):
+        if self.order == "reference" or isinstance(input, gs.DeviceCSR) or sps.issparse(input):
+            return super().forward(input, target_indices=target_indices, **kwargs)
+        P = self.propagate(input, target_indices)  # (H . h)[rows], K wide
         Y = torch.addmm(self.b, P, self.W) if self.b is not None else P @ self.W
         if self.fused_act == "relu":
             Y = torch.relu(Y)

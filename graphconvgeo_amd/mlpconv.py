@@ -5,8 +5,12 @@ Same constructor, `fit(X, train_indices, dev_indices, test_indices, Y, H)`,
 step over all N nodes (mlpconv.py:293-295):
 
   forward   Z1 = X.W1 (HIP SpMM)  h = rectify(H.Z1 + b1) (HIP SpMM, fused epilogue)
-            Z2 = h.W2 (fp32 GEMM)  logits = (H.Z2 + b2)[train_indices] (HIP SpMM, fused rows)
-  loss      mean categorical CE of softmax(logits) + L1/L2 shares on W (mlpconv.py:228-245)
+            order "reference": Z2 = h.W2 (fp32 GEMM), logits = (H.Z2 + b2)[train_indices]
+              (HIP SpMM, fused rows), then the softmax-CE row kernel (loss, hits; gradient pass
+              in backward)
+            order "propagate_first": P = (H.h)[train_indices] (HIP SpMM), then ONE MFMA kernel
+              for P.W2 + b2, softmax, CE, argmax hits and the logits gradient (csrc/dense.hip)
+  loss      mean categorical CE of softmax(logits) + L1/L2 shares on W (mlpconv.py:229-243)
   backward  Theano's rules through the HIP kernels (scatter-add, H.g, X^T.g)
   update    lasagne.updates.adam(lr=4e-3, 0.9, 0.999, 1e-8) (mlpconv.py:263), restated below
             (its epsilon sits outside the bias correction, unlike torch.optim.Adam)
@@ -26,6 +30,7 @@ from typing import Optional
 import numpy as np
 import torch
 
+from . import dense
 from . import sparse as gs
 from .layers import ConvolutionDenseLayer, SparseConvolutionDenseLayer
 
@@ -135,10 +140,22 @@ class MLPCONV:
                 self.l_hid1.b.copy_(torch.as_tensor(self.init_parameters[1]))
                 self.l_out.b.copy_(torch.as_tensor(self.init_parameters[3]))
         self.params = [self.l_hid1.W, self.l_hid1.b, self.l_out.W, self.l_out.b]
+        self._proj = dense.Projection()  # padded W2 copies for the fused MFMA output kernel
+
+    def _fused_output(self) -> bool:
+        return self.l_out.order == "propagate_first" and \
+            self.l_out.num_units <= dense.FUSED_MAX_COLS
 
     def _logits(self, rows: gs.RowSelection) -> torch.Tensor:
         h = self.l_hid1(self.Xd)
         return self.l_out(h, target_indices=rows)  # (H.(h.W2) + b2)[rows], pre-softmax
+
+    def _probabilities(self, rows: gs.RowSelection) -> torch.Tensor:
+        h = self.l_hid1(self.Xd)
+        if self._fused_output():
+            return self._proj.probabilities(self.l_out.propagate(h, rows), self.l_out.W,
+                                            self.l_out.b)
+        return dense.softmax(self.l_out(h, target_indices=rows))
 
     def _penalty(self) -> torch.Tensor:
         c_out, c_hid = self.regul_coefs
@@ -147,12 +164,16 @@ class MLPCONV:
                 + W1.abs().sum() * (c_hid * 0.5) + (W1 * W1).sum() * (c_hid * 0.5))
 
     def _loss_acc(self, rows: gs.RowSelection, y: torch.Tensor, penalty: bool = True):
-        logits = self._logits(rows)
-        logp = torch.log_softmax(logits, dim=1)
-        loss = -logp.gather(1, y.view(-1, 1)).mean()
+        """categorical_crossentropy(softmax(logits), y).mean() (+ penalty) and the argmax
+        accuracy (mlpconv.py:227-253), through the HIP softmax-CE kernels."""
+        h = self.l_hid1(self.Xd)
+        if self._fused_output():
+            P = self.l_out.propagate(h, rows)  # (H . h)[rows], K wide
+            loss, acc = self._proj.softmax_xent(P, self.l_out.W, self.l_out.b, y)
+        else:
+            loss, acc = dense.softmax_xent(self.l_out(h, target_indices=rows), y)
         if penalty:
             loss = loss + self._penalty()
-        acc = (logits.argmax(dim=1) == y).float().mean()
         return loss, acc
 
     # -- reference API ------------------------------------------------------------------
@@ -171,8 +192,8 @@ class MLPCONV:
         self.rows = {k: gs.RowSelection(v, self.device) for k, v in
                      (("train", self.train_indices), ("dev", self.dev_indices),
                       ("test", self.test_indices))}
-        y_train = torch.as_tensor(Y[self.train_indices].astype(np.int64), device=self.device)
-        y_dev = torch.as_tensor(Y[self.dev_indices].astype(np.int64), device=self.device)
+        y_train = torch.as_tensor(Y[self.train_indices].astype(np.int32), device=self.device)
+        y_dev = torch.as_tensor(Y[self.dev_indices].astype(np.int32), device=self.device)
         opt = LasagneAdam(self.params, lr=4e-3, beta1=0.9, beta2=0.999, epsilon=1e-8)
         self.optimizer = opt
         train_step = self._make_train_step(opt, y_train)
@@ -259,16 +280,16 @@ class MLPCONV:
 
     @torch.no_grad()
     def predict_proba(self, dataset_partition):
-        return torch.softmax(self._logits(self._indices(dataset_partition)), dim=1).cpu().numpy()
+        return self._probabilities(self._indices(dataset_partition)).cpu().numpy()
 
     @torch.no_grad()
     def predict(self, dataset_partition):
-        return self._logits(self._indices(dataset_partition)).argmax(dim=1).cpu().numpy()
+        return self._probabilities(self._indices(dataset_partition)).argmax(dim=1).cpu().numpy()
 
     @torch.no_grad()
     def accuracy(self, dataset_partition, y_true):
         rows = self._indices(dataset_partition)
-        y = torch.as_tensor(np.asarray(y_true).astype(np.int64), device=self.device)
+        y = torch.as_tensor(np.asarray(y_true).astype(np.int32), device=self.device)
         _loss, acc = self._loss_acc(rows, y)
         return float(acc)
 

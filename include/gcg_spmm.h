@@ -213,6 +213,53 @@ gcg_status gcg_project_mention_graph(int64_t n_targets, int64_t n_nodes, int64_t
                                      int32_t* out_u, int32_t* out_v, int64_t capacity,
                                      int64_t* n_edges, int32_t* status_dev, gcg_stream_t stream);
 
+/*
+ * Dense side of the output layer on the matrix cores (v_mfma_f32_16x16x4_f32: f32 in, f32
+ * accumulate; the k order inside a 16-deep step is permuted, so results equal a BLAS sgemm
+ * within f32 rounding, not bit for bit). Row-major operands; A: M x K (lda), B: K x N (ldb),
+ * C: M x N (ldc). A and B need 16-B aligned bases and ld % 4 == 0; B is read at columns
+ * < round4(N), so ldb >= round4(N) (pad the weight, as graphconvgeo_amd.dense does).
+ *
+ * gcg_gemm_f32: C = act(A . B + bias)        T.dot(h, W) (+ b) at mlpconv.py:88 / the
+ *   propagate-first form of mlpconv.py:88-93, and Theano's g . W^T (W^T passed as B).
+ */
+gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                        const float* B, int64_t ldb, const float* bias /*nullable*/, int act,
+                        float* C, int64_t ldc, gcg_stream_t stream);
+
+/*
+ * Fused output layer + loss (N <= 1024; one workgroup owns whole rows):
+ *   logits = A . W + bias                                       mlpconv.py:88-93
+ *   labels != NULL: out = (softmax(logits) - onehot(labels)) * scale   (the logits gradient
+ *     of categorical_crossentropy(...).mean() with scale = 1/M, mlpconv.py:229-230),
+ *     loss_rows[i] = -log softmax(logits)[i, labels[i]],
+ *     correct_rows[i] (nullable) = 1 if the first-index argmax equals labels[i] else 0
+ *     (argmax + T.eq accuracy, mlpconv.py:227,252);
+ *   labels == NULL: out = softmax(logits) (predict_proba, mlpconv.py:329-335);
+ *   out may be NULL when labels are given (evaluation: loss and accuracy only).
+ * scale_dev (nullable, device): multiplies scale (the upstream gradient of the loss, read
+ * on the device so the call can sit inside a captured HIP graph). The logits never reach HBM.
+ */
+gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
+                                        int64_t lda, const float* W, int64_t ldw,
+                                        const float* bias /*nullable*/,
+                                        const int32_t* labels /*nullable*/, float scale,
+                                        const float* scale_dev /*nullable*/,
+                                        float* out /*nullable*/, int64_t ldo, float* loss_rows,
+                                        float* correct_rows /*nullable*/, gcg_stream_t stream);
+
+/*
+ * The same row epilogue for logits that already exist (the reference order, where the
+ * logits are the H SpMM's output rows, mlpconv.py:90-94): one wave per row, N <= 4096,
+ * out may alias logits; out == NULL computes loss_rows / correct_rows only (the forward
+ * half; the gradient pass then runs with out set and scale_dev = the upstream gradient).
+ */
+gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
+                                const int32_t* labels /*nullable*/, float scale,
+                                const float* scale_dev /*nullable*/, float* out /*nullable*/,
+                                int64_t ldo, float* loss_rows, float* correct_rows /*nullable*/,
+                                gcg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

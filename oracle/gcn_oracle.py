@@ -145,6 +145,27 @@ def softmax(x):
     return e / e.sum(axis=1, keepdims=True)
 
 
+def softmax_xent_f64(logits, y=None, scale=None):
+    """float64 restatement of the output-layer loss: softmax (mlpconv.py:95), per-row
+    categorical cross-entropy -log softmax[i, y_i] (mlpconv.py:229), hit = argmax == y with
+    numpy's first-index argmax (mlpconv.py:227,252), and the logits gradient of the mean
+    loss, (softmax - onehot) * scale with scale = 1/M (Theano's crossentropy_softmax grad).
+    Returns (probabilities, loss_rows, hits, grad); the last three are None without y."""
+    x = np.asarray(logits, dtype=np.float64)
+    P = softmax(x)
+    if y is None:
+        return P, None, None, None
+    y = np.asarray(y)
+    r = np.arange(x.shape[0])
+    m = x.max(axis=1)
+    loss = (m + np.log(np.exp(x - m[:, None]).sum(axis=1))) - x[r, y]
+    hits = (x.argmax(axis=1) == y).astype(np.float64)
+    G = P.copy()
+    G[r, y] -= 1.0
+    G *= (1.0 / max(x.shape[0], 1)) if scale is None else scale
+    return P, loss, hits, G
+
+
 def gcn_forward(X, H, W1, b1, W2, b2, idx, dtype=np.float64):
     """Returns dict of intermediates: Z1, pre1, h, Z2, pre2, logits (= pre2[idx]), P."""
     if dtype == np.float32:

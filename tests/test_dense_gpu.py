@@ -1,0 +1,171 @@
+"""GPU parity of the MFMA dense kernels (csrc/dense.hip): the output layer's T.dot(h, W) + b
+(mlpconv.py:88-93), softmax / categorical cross-entropy / accuracy (mlpconv.py:227-253)
+and their gradients, against float64 restatements (oracle.gcn_oracle.softmax_xent_f64).
+
+Tolerances (fp32 MFMA = exact f32 products, f32 accumulation in a permuted k order):
+  GEMM        |C - C64| <= 2e-6 * (|A| @ |B|) + 1e-30   (a few ulps of the absolute sum)
+  softmax/CE  |.| <= 1e-5 (probabilities / gradients <= 1 in magnitude, K <= 1024)
+"""
+import numpy as np
+import pytest
+import torch
+
+from graphconvgeo_amd import dense
+from graphconvgeo_amd.sparse import empty_dense
+from oracle import gcn_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+def _rand(shape, seed, scale=1.0):
+    return (np.random.default_rng(seed).standard_normal(shape) * scale).astype(np.float32)
+
+
+def _check_gemm(C, A, B, bias=None, relu=False):
+    C64 = A.astype(np.float64) @ B.astype(np.float64)
+    if bias is not None:
+        C64 = C64 + bias.astype(np.float64)
+    if relu:
+        C64 = np.maximum(C64, 0)
+    bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+                    + (0 if bias is None else np.abs(bias))) + 1e-30
+    err = np.abs(C.astype(np.float64) - C64)
+    assert (err <= bound).all(), f"max err {err.max()} (bound at worst {bound.ravel()[err.argmax()]})"
+
+
+def _padded(W, dev, transpose=False):
+    return dense._WeightCache().get(torch.from_numpy(W).to(dev), transpose)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 1, 1), (5, 3, 7), (33, 16, 64), (64, 17, 65),
+                                   (100, 64, 129), (257, 300, 256), (130, 300, 300),
+                                   (70, 300, 321), (96, 300, 930), (40, 930, 300),
+                                   (31, 65, 1024), (50, 40, 1500), (300, 129, 4)])
+def test_gemm_vs_float64(cuda, M, K, N):
+    A, B = _rand((M, K), 1), _rand((K, N), 2)
+    C = dense.gemm(torch.from_numpy(A).to(cuda), _padded(B, cuda)).cpu().numpy()
+    _check_gemm(C, A, B)
+
+
+def test_gemm_bias_relu_and_strided(cuda):
+    M, K, N = 200, 300, 930
+    A, B, b = _rand((M, K), 3), _rand((K, N), 4), _rand((N,), 5)
+    At = torch.from_numpy(A).to(cuda)
+    bt = torch.from_numpy(b).to(cuda)
+    C = dense.gemm(At, _padded(B, cuda), bias=bt, act="relu").cpu().numpy()
+    _check_gemm(C, A, B, bias=b, relu=True)
+    # A with a leading dimension that is not a multiple of 4 is re-laid out, same result
+    big = torch.zeros((M, K + 3), device=cuda)
+    big[:, :K] = At
+    C2 = dense.gemm(big[:, :K], _padded(B, cuda), bias=bt, act="relu").cpu().numpy()
+    assert np.array_equal(C, C2)
+    # output into a caller-owned padded buffer
+    out = empty_dense(M, N, cuda)
+    dense.gemm(At, _padded(B, cuda), bias=bt, act="relu", out=out)
+    assert np.array_equal(out.cpu().numpy(), C)
+
+
+def test_gemm_exact_integer_layout(cuda):
+    """Small-integer operands: every product and sum is exact in f32, so any lane/row/column
+    mix-up shows as an exact mismatch (asymmetric B)."""
+    rng = np.random.default_rng(7)
+    M, K, N = 77, 45, 330
+    A = rng.integers(-3, 4, (M, K)).astype(np.float32)
+    B = rng.integers(-3, 4, (K, N)).astype(np.float32)
+    B[0, :] = np.arange(N)  # asymmetric
+    C = dense.gemm(torch.from_numpy(A).to(cuda), _padded(B, cuda)).cpu().numpy()
+    assert np.array_equal(C, (A.astype(np.int64) @ B.astype(np.int64)).astype(np.float32))
+
+
+def test_gemm_rejects_bad_operands(cuda):
+    A = torch.randn(8, 12, device=cuda)
+    with pytest.raises(ValueError):
+        dense.gemm(A, torch.randn(12, 10, device=cuda))  # ld 10 < round4(10) = 12
+    with pytest.raises(ValueError):
+        dense.gemm(A, torch.randn(11, 12, device=cuda))
+    with pytest.raises(ValueError):
+        dense.gemm(A.cpu(), torch.randn(12, 12))
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 4, 2), (37, 16, 129), (300, 300, 256), (513, 300, 930),
+                                   (64, 65, 1024), (20, 3, 61)])
+def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
+    P, W, b = _rand((M, K), 11, 0.3), _rand((K, N), 12, 0.3), _rand((N,), 13)
+    y = np.random.default_rng(14).integers(0, N, M).astype(np.int32)
+    proj = dense.Projection()
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    G = empty_dense(M, N, cuda)
+    loss = torch.empty(M, device=cuda)
+    hits = torch.empty(M, device=cuda)
+    dense._fused(Pt, proj.fwd.get(Wt, False), bt, yt, 1.0 / M, None, G, loss, hits)
+    logits64 = P.astype(np.float64) @ W.astype(np.float64) + b
+    P64, loss64, hits64, G64 = O.softmax_xent_f64(logits64, y)
+    assert np.abs(loss.cpu().numpy() - loss64).max() < 1e-5
+    assert np.abs(G.cpu().numpy() - G64).max() < 1e-5 / M + 1e-7
+    # hits: compare where the top-2 margin is clearly above f32 rounding
+    srt = np.sort(logits64, axis=1)
+    clear = (srt[:, -1] - srt[:, -2] if N > 1 else np.ones(M)) > 1e-4
+    assert np.array_equal(hits.cpu().numpy()[clear], hits64[clear])
+    probs = proj.probabilities(Pt, Wt, bt).cpu().numpy()
+    assert np.abs(probs - P64).max() < 1e-5
+    # loss-only evaluation (no gradient written)
+    loss2 = torch.empty(M, device=cuda)
+    dense._fused(Pt, proj.fwd.get(Wt, False), bt, yt, 1.0, None, None, loss2, None)
+    assert torch.equal(loss, loss2)
+
+
+def test_rows_softmax_xent_vs_float64(cuda):
+    for M, N in [(1, 1), (9, 3), (1000, 930), (257, 256), (33, 4096), (5, 1025)]:
+        L = _rand((M, N), M + N, 3.0)
+        y = np.random.default_rng(M).integers(0, N, M).astype(np.int32)
+        Lt = torch.from_numpy(L).to(cuda)
+        P64, loss64, hits64, G64 = O.softmax_xent_f64(L, y)
+        loss, acc = dense.softmax_xent(Lt, torch.from_numpy(y).to(cuda))
+        assert abs(float(loss) - loss64.mean()) < 1e-5 * max(1.0, abs(loss64.mean()))
+        assert abs(float(acc) - hits64.mean()) < 1.5 / M
+        probs = dense.softmax(Lt).cpu().numpy()
+        assert np.abs(probs - P64).max() < 1e-5
+
+
+def test_project_xent_autograd_vs_float64(cuda):
+    M, K, N = 400, 300, 129
+    P, W, b = _rand((M, K), 21, 0.2), _rand((K, N), 22, 0.2), _rand((N,), 23, 0.1)
+    y = np.random.default_rng(24).integers(0, N, M)
+    Pt = torch.from_numpy(P).to(cuda).requires_grad_()
+    Wt = torch.from_numpy(W).to(cuda).requires_grad_()
+    bt = torch.from_numpy(b).to(cuda).requires_grad_()
+    loss, acc = dense.project_softmax_xent(Pt, Wt, bt, torch.from_numpy(y).to(cuda))
+    (loss * 2.5).backward()  # upstream gradient != 1 goes through the folded scale
+    logits64 = P.astype(np.float64) @ W + b
+    _, loss64, hits64, G64 = O.softmax_xent_f64(logits64, y)
+    G64 = G64 * 2.5
+    assert abs(float(loss) - loss64.mean()) < 1e-5
+    assert np.abs(Pt.grad.cpu().numpy() - G64 @ W.T.astype(np.float64)).max() < 1e-6
+    assert np.abs(Wt.grad.cpu().numpy() - P.T.astype(np.float64) @ G64).max() < 1e-5
+    assert np.abs(bt.grad.cpu().numpy() - G64.sum(0)).max() < 1e-5
+
+
+def test_rows_xent_autograd_and_matmul_autograd(cuda):
+    M, K, N = 300, 64, 200
+    A, W, b = _rand((M, K), 31, 0.3), _rand((K, N), 32, 0.3), _rand((N,), 33, 0.1)
+    y = np.random.default_rng(34).integers(0, N, M)
+    proj = dense.Projection()
+    At = torch.from_numpy(A).to(cuda).requires_grad_()
+    Wt = torch.from_numpy(W).to(cuda).requires_grad_()
+    bt = torch.from_numpy(b).to(cuda).requires_grad_()
+    logits = proj.matmul(At, Wt, bt)
+    loss, _ = dense.softmax_xent(logits, torch.from_numpy(y).to(cuda))
+    (0.5 * loss).backward()
+    _, loss64, _, G64 = O.softmax_xent_f64(A.astype(np.float64) @ W + b, y)
+    G64 *= 0.5
+    assert abs(float(loss) - loss64.mean()) < 1e-5
+    assert np.abs(At.grad.cpu().numpy() - G64 @ W.T.astype(np.float64)).max() < 1e-6
+    assert np.abs(Wt.grad.cpu().numpy() - A.T.astype(np.float64) @ G64).max() < 1e-6
+    assert np.abs(bt.grad.cpu().numpy() - G64.sum(0)).max() < 1e-6
+
+
+def test_fused_rejects_too_many_classes(cuda):
+    with pytest.raises(ValueError):
+        dense.project_softmax_xent(torch.randn(4, 8, device=cuda), torch.randn(8, 1025, device=cuda),
+                                   None, torch.zeros(4, dtype=torch.int64, device=cuda))
