@@ -63,19 +63,20 @@ __device__ __forceinline__ int reduce16_min(int v) {
 
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 
-template <int RT, int G, int WR, int WC, int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_kernel(
+template <int RT, int G, int WR, int WC, int EPI, int PF>
+__global__ __launch_bounds__(64 * WR * WC, 1) void gemm_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
     float* __restrict__ loss_rows, float* __restrict__ correct_rows) {
-  static_assert(WR * WC == 4, "4 waves per workgroup");
+  constexpr int NT = 64 * WR * WC;  // threads per workgroup (4 or 8 waves)
+  static_assert(WR * WC == 4 || WR * WC == 8, "4 or 8 waves per workgroup");
   constexpr int BM = 16 * RT * WR;
   constexpr int BN = 64 * G * WC;
   constexpr int KC = 32;                   // k depth of one LDS chunk
   constexpr int KP = KC + 4;               // padded LDS row (floats)
-  constexpr int A4 = BM * KC / 4 / 256;    // A dwordx4 per thread per chunk
-  static_assert(A4 >= 1 && BM * KC / 4 % 256 == 0, "A chunk must split evenly");
+  constexpr int A4 = BM * KC / 4 / NT;     // A dwordx4 per thread per chunk
+  static_assert(A4 >= 1 && BM * KC / 4 % NT == 0, "A chunk must split evenly");
   __shared__ float As[2][BM][KP];
   __shared__ float red[3][WC][BM];
 
@@ -115,7 +116,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
   auto load_a = [&](int kc0) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int r = idx / (KC / 4), k = kc0 + (idx % (KC / 4)) * 4;
       const int64_t gr = row0 + r;
       const int64_t rr = gr < M ? gr : M - 1;
@@ -132,7 +133,7 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
   auto store_a = [&](int buf) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
-      const int idx = tid + 256 * i;
+      const int idx = tid + NT * i;
       const int r = idx / (KC / 4), k4 = (idx % (KC / 4)) * 4;
       *reinterpret_cast<f4*>(&As[buf][r][k4]) = areg[i];
     }
@@ -187,18 +188,37 @@ __global__ __launch_bounds__(256, 1) void gemm_kernel(
   load_a(0);
   store_a(0);
   lds_barrier();
-  f4 b0[G][4], b1[G][4];
-  load_b(b0, 0);
-  for (int c = 0; c < n_chunks; ++c) {
-    const int buf = c & 1;
-    const int k0 = c * KC;
-    load_a(k0 + KC);  // past K: clamped and zeroed, never used
-    load_b(b1, k0 + 16);
-    compute(b0, buf, 0);
-    load_b(b0, k0 + 32);
-    if (k0 + 16 < K) compute(b1, buf, 1);
-    store_a(buf ^ 1);
-    lds_barrier();
+  f4 b0[G][4];
+  if constexpr (PF) {
+    f4 b1[G][4];
+    load_b(b0, 0);
+    for (int c = 0; c < n_chunks; ++c) {
+      const int buf = c & 1;
+      const int k0 = c * KC;
+      load_a(k0 + KC);  // past K: clamped and zeroed, never used
+      load_b(b1, k0 + 16);
+      compute(b0, buf, 0);
+      load_b(b0, k0 + 32);
+      if (k0 + 16 < K) compute(b1, buf, 1);
+      store_a(buf ^ 1);
+      lds_barrier();
+    }
+  } else {
+    // One B register set: a wave waits for its step's loads while the other wave(s) on
+    // its SIMD compute (8-wave workgroups, 2 waves per SIMD).
+    for (int c = 0; c < n_chunks; ++c) {
+      const int buf = c & 1;
+      const int k0 = c * KC;
+      load_a(k0 + KC);
+      load_b(b0, k0);
+      compute(b0, buf, 0);
+      if (k0 + 16 < K) {
+        load_b(b0, k0 + 16);
+        compute(b0, buf, 1);
+      }
+      store_a(buf ^ 1);
+      lds_barrier();
+    }
   }
 
   // ---- epilogue ----
@@ -461,7 +481,9 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
                        float* correct_rows) {
 #define GCG_GEMM_CASE(rt, g, wr, wc)                                                        \
   if (s.RT == rt && s.G == g && s.WR == wr && s.WC == wc) {                                  \
-    hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI>), grid, dim3(256), 0, st, M, N, K, A, \
+    constexpr int pf = (wr) * (wc) == 4 ? 1 : 0;                                             \
+    hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI, pf>), grid, dim3(64 * (wr) * (wc)), 0, \
+                       st, M, N, K, A,                                                       \
                        lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
                        correct_rows);                                                         \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
@@ -474,6 +496,8 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
   GCG_GEMM_CASE(4, 4, 1, 4)
   GCG_GEMM_CASE(4, 2, 1, 4)
   GCG_GEMM_CASE(4, 3, 1, 4)
+  GCG_GEMM_CASE(2, 4, 2, 4)
+  GCG_GEMM_CASE(2, 2, 2, 4)
   GCG_GEMM_CASE(2, 1, 4, 1)
   GCG_GEMM_CASE(2, 2, 4, 1)
   GCG_GEMM_CASE(2, 3, 4, 1)
@@ -495,6 +519,7 @@ Shape pick_shape(int64_t N, bool fused) {
   const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
   if (fused || groups > 5) {
     const int g = std::min(4, (groups + 3) / 4);
+    if (env_int("GCG_GEMM_8W") && (g == 4 || g == 2)) return Shape{2, g, 2, 4};  // experiment
     return Shape{g >= 2 ? rt : 2, std::max(g, 1), 1, 4};
   }
   return Shape{2, std::max(groups, 1), 4, 1};

@@ -155,3 +155,37 @@ def test_plain_c_consumer(native_lib, tmp_path):
     res = subprocess.run([str(exe)], capture_output=True, text=True)
     assert res.returncode == 0, (res.returncode, res.stdout, res.stderr)
     assert "abi ok" in res.stdout
+
+
+def test_dense_abi_argument_validation_without_gpu(native_lib):
+    """The MFMA dense entry points (csrc/dense.hip) reject bad shapes, layouts and missing
+    outputs before any launch: sizes, 16-B alignment / ld % 4 of the dwordx4 operands,
+    ldb >= round4(N), the fused kernel's 1024-class row limit, the row kernel's 4096."""
+    import ctypes as C
+    lib = native_lib
+    a16, b16, c16 = C.c_void_p(0x10000), C.c_void_p(0x20000), C.c_void_p(0x30000)
+    odd = C.c_void_p(0x10004)  # 4-B but not 16-B aligned
+    st = {"ok": 0, "inval": 1, "mis": 2}
+    gemm = lib.gcg_gemm_f32
+    assert gemm(-1, 4, 4, a16, 4, b16, 4, None, 0, c16, 4, None) == st["inval"]
+    assert gemm(4, 0, 4, a16, 4, b16, 4, None, 0, c16, 4, None) == st["inval"]
+    assert gemm(4, 4, 4, None, 4, b16, 4, None, 0, c16, 4, None) == st["inval"]
+    assert gemm(4, 4, 4, a16, 4, b16, 4, None, 7, c16, 4, None) == st["inval"]   # act
+    assert gemm(4, 4, 8, a16, 4, b16, 4, None, 0, c16, 4, None) == st["inval"]   # lda < K
+    assert gemm(4, 6, 4, a16, 4, b16, 6, None, 0, c16, 8, None) == st["inval"]   # ldb < round4(N)
+    assert gemm(4, 4, 4, odd, 4, b16, 4, None, 0, c16, 4, None) == st["mis"]
+    assert gemm(4, 4, 6, a16, 6, b16, 4, None, 0, c16, 4, None) == st["mis"]     # lda % 4
+    assert gemm(0, 4, 4, a16, 4, b16, 4, None, 0, c16, 4, None) == st["ok"]      # M = 0: no-op
+    fused = lib.gcg_project_softmax_xent_f32
+    lab, loss = C.c_void_p(0x40000), C.c_void_p(0x50000)
+    assert fused(4, 1025, 4, a16, 4, b16, 1028, None, lab, 1.0, None, c16, 1028, loss, None,
+                 None) == st["inval"]
+    assert fused(4, 8, 4, a16, 4, b16, 8, None, lab, 1.0, None, c16, 8, None, None,
+                 None) == st["inval"]                                           # no loss_rows
+    assert fused(0, 8, 4, a16, 4, b16, 8, None, lab, 1.0, None, None, 0, loss, None,
+                 None) == st["ok"]                                              # eval form, M = 0
+    rows = lib.gcg_softmax_xent_f32
+    assert rows(4, 4097, a16, 4100, lab, 1.0, None, c16, 4100, loss, None, None) == st["inval"]
+    assert rows(4, 8, a16, 8, None, 1.0, None, None, 8, None, None, None) == st["inval"]
+    assert rows(4, 8, a16, 4, lab, 1.0, None, None, 8, loss, None, None) == st["inval"]  # ldl < N
+    assert "gcg_softmax_xent_f32" in lib.gcg_last_error().decode()

@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=300)
     ap.add_argument("--classes", type=int, default=930)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--rt", default="2,4", help="GCG_GEMM_RT values to compare")
+    ap.add_argument("--tiles", default="rt2,rt4,8w", help="wide-tile variants to compare")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     T, N, K, C = args.rows, args.nodes, args.hidden, args.classes
@@ -86,11 +86,14 @@ def main():
     def ours_fused():
         dense._fused(P, Wp, b, y32, 1.0 / T, None, G, loss, hits)
 
-    for rt in args.rt.split(","):  # GCG_GEMM_RT: row tiles per wave of the wide tiles
-        os.environ["GCG_GEMM_RT"] = rt
-        rec(f"proj P.W2+b2 RT={rt}", time_op(lambda: dense.gemm(P, Wp, bias=b, out=out), args.reps), f)
-        rec(f"fused RT={rt}", time_op(ours_fused, args.reps), f)
-    os.environ.pop("GCG_GEMM_RT", None)
+    knobs = {"rt2": {"GCG_GEMM_RT": "2"}, "rt4": {"GCG_GEMM_RT": "4"}, "8w": {"GCG_GEMM_8W": "1"}}
+    for name in args.tiles.split(","):  # wide-tile variants (experiment knobs of dense.hip)
+        for k, v in knobs[name].items():
+            os.environ[k] = v
+        rec(f"proj P.W2+b2 {name}", time_op(lambda: dense.gemm(P, Wp, bias=b, out=out), args.reps), f)
+        rec(f"fused {name}", time_op(ours_fused, args.reps), f)
+        for k in knobs[name]:
+            os.environ.pop(k, None)
     rec("proj P.W2+b2", time_op(lambda: dense.gemm(P, Wp, bias=b, out=out), args.reps), f,
         time_op(lambda: torch.addmm(b, P, W), args.reps))
 
