@@ -64,7 +64,7 @@ __device__ __forceinline__ int reduce16_min(int v) {
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 
 template <int RT, int G, int WR, int WC, int EPI, int PF>
-__global__ __launch_bounds__(64 * WR * WC, 1) void gemm_kernel(
+__global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void gemm_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
@@ -96,7 +96,6 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void gemm_kernel(
     const int c = colw + 64 * g + 4 * j;
     bcol[g] = c < n4 ? c : 0;
   }
-  const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
 
   f4 acc[RT][G][4];
 #pragma unroll
@@ -159,6 +158,11 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void gemm_kernel(
   };
 
   const int arow = wr * 16 * RT + j;
+  // Skipping groups past N (a wave-uniform branch per step and group) measured faster with the
+  // register-prefetch (PF = 1) body -- without it hipcc shuffles the accumulators through
+  // AGPR copies and spills -- and slower with the single-buffer body.
+  constexpr bool SKIP = PF != 0;
+  const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
   auto compute = [&](const f4 (&bf)[G][4], int buf, int s) {
     f4 af[RT];
 #pragma unroll
@@ -168,7 +172,7 @@ __global__ __launch_bounds__(64 * WR * WC, 1) void gemm_kernel(
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
-        if (g >= ngv) continue;  // scalar branch: group entirely past N
+        if (SKIP && g >= ngv) continue;  // scalar branch: group entirely past N
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
           acc[t][g][0] = mfma4(af[t][e], bf[g][e].x, acc[t][g][0]);
@@ -466,7 +470,7 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 // ---------------------------------------------------------------------------------------
 
 struct Shape {
-  int RT, G, WR, WC;
+  int RT, G, WR, WC, PF = 1;
   int bm() const { return 16 * RT * WR; }
   int bn() const { return 64 * G * WC; }
 };
@@ -479,9 +483,8 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
                        const float* bias, int act, float* C, int64_t ldc, const int32_t* labels,
                        float scale, const float* scale_dev, float* loss_rows,
                        float* correct_rows) {
-#define GCG_GEMM_CASE(rt, g, wr, wc)                                                        \
-  if (s.RT == rt && s.G == g && s.WR == wr && s.WC == wc) {                                  \
-    constexpr int pf = (wr) * (wc) == 4 ? 1 : 0;                                             \
+#define GCG_GEMM_CASE(rt, g, wr, wc, pf)                                                    \
+  if (s.RT == rt && s.G == g && s.WR == wr && s.WC == wc && s.PF == pf) {                    \
     hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI, pf>), grid, dim3(64 * (wr) * (wc)), 0, \
                        st, M, N, K, A,                                                       \
                        lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
@@ -489,23 +492,25 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
-  GCG_GEMM_CASE(2, 1, 1, 4)
-  GCG_GEMM_CASE(2, 2, 1, 4)
-  GCG_GEMM_CASE(2, 3, 1, 4)
-  GCG_GEMM_CASE(2, 4, 1, 4)
-  GCG_GEMM_CASE(4, 4, 1, 4)
-  GCG_GEMM_CASE(4, 2, 1, 4)
-  GCG_GEMM_CASE(4, 3, 1, 4)
-  GCG_GEMM_CASE(2, 4, 2, 4)
-  GCG_GEMM_CASE(2, 2, 2, 4)
-  GCG_GEMM_CASE(2, 1, 4, 1)
-  GCG_GEMM_CASE(2, 2, 4, 1)
-  GCG_GEMM_CASE(2, 3, 4, 1)
-  GCG_GEMM_CASE(2, 4, 4, 1)
-  GCG_GEMM_CASE(2, 5, 4, 1)
+  GCG_GEMM_CASE(2, 1, 1, 4, 1)
+  GCG_GEMM_CASE(2, 2, 1, 4, 1)
+  GCG_GEMM_CASE(2, 3, 1, 4, 1)
+  GCG_GEMM_CASE(2, 4, 1, 4, 1)
+  GCG_GEMM_CASE(4, 4, 1, 4, 1)
+  GCG_GEMM_CASE(4, 2, 1, 4, 1)
+  GCG_GEMM_CASE(4, 3, 1, 4, 1)
+  GCG_GEMM_CASE(2, 4, 1, 4, 0)
+  GCG_GEMM_CASE(2, 2, 1, 4, 0)
+  GCG_GEMM_CASE(2, 3, 1, 4, 0)
+  GCG_GEMM_CASE(2, 4, 2, 4, 0)
+  GCG_GEMM_CASE(2, 1, 4, 1, 1)
+  GCG_GEMM_CASE(2, 2, 4, 1, 1)
+  GCG_GEMM_CASE(2, 3, 4, 1, 1)
+  GCG_GEMM_CASE(2, 4, 4, 1, 1)
+  GCG_GEMM_CASE(2, 5, 4, 1, 1)
 #undef GCG_GEMM_CASE
-  return fail(GCG_ERR_INVALID_ARG, "gemm: no tile instantiated for RT=%d G=%d WR=%d WC=%d", s.RT,
-              s.G, s.WR, s.WC);
+  return fail(GCG_ERR_INVALID_ARG, "gemm: no tile instantiated for RT=%d G=%d WR=%d WC=%d PF=%d",
+              s.RT, s.G, s.WR, s.WC, s.PF);
 }
 
 // Tile choice. fused: the workgroup must hold the whole row (WC = 4, G = ceil(N/256)).
@@ -513,13 +518,20 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
 // wider N -> row bands of 32 rows x up to 1024 columns, grid.y for the rest.
 Shape pick_shape(int64_t N, bool fused) {
   const int groups = static_cast<int>((N + 63) / 64);
-  // Row tiles per wave of the wide (WC = 4) tiles: 4 (64-row workgroups) halves the L2 traffic
-  // of B per flop; measured 92.6 vs 83.2 TFLOP/s (plain) and 78.6 vs 72.3 (fused) on
-  // Twitter-World's 840k x 300 x 930. GCG_GEMM_RT=2 selects the smaller tile (experiments).
+  // Wide (WC = 4) tiles, measured on Twitter-World's 840k x 300 x 930 (TFLOP/s, plain / fused):
+  //   RT = 4, B ping-pong, 1 workgroup per CU          92.8 / 78.7   <- plain default
+  //   RT = 2, B ping-pong, 1 workgroup per CU          83.0 / 72.2
+  //   RT = 2, one B set, 2 workgroups per CU           91.8 / 85.0   <- fused default: the
+  //       second workgroup hides B latency and overlaps the other's softmax epilogue + stores
+  //   RT = 2, one B set, 8-wave workgroup              93.1 / 83.8
+  // Knobs for experiments: GCG_GEMM_RT=2, GCG_GEMM_8W=1, GCG_GEMM_OCC2=0/1.
   const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
   if (fused || groups > 5) {
     const int g = std::min(4, (groups + 3) / 4);
-    if (env_int("GCG_GEMM_8W") && (g == 4 || g == 2)) return Shape{2, g, 2, 4};  // experiment
+    if (env_int("GCG_GEMM_8W") && g == 4) return Shape{2, 4, 2, 4, 0};
+    const char* occ = std::getenv("GCG_GEMM_OCC2");
+    const bool occ2 = occ ? std::atoi(occ) != 0 : fused;
+    if (occ2 && g >= 2) return Shape{2, g, 1, 4, 0};
     return Shape{g >= 2 ? rt : 2, std::max(g, 1), 1, 4};
   }
   return Shape{2, std::max(groups, 1), 4, 1};

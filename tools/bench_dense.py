@@ -49,7 +49,7 @@ def main():
     ap.add_argument("--hidden", type=int, default=300)
     ap.add_argument("--classes", type=int, default=930)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--tiles", default="rt2,rt4,8w", help="wide-tile variants to compare")
+    ap.add_argument("--tiles", default="rt2,rt4,8w,occ2", help="wide-tile variants to compare")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     T, N, K, C = args.rows, args.nodes, args.hidden, args.classes
@@ -86,7 +86,9 @@ def main():
     def ours_fused():
         dense._fused(P, Wp, b, y32, 1.0 / T, None, G, loss, hits)
 
-    knobs = {"rt2": {"GCG_GEMM_RT": "2"}, "rt4": {"GCG_GEMM_RT": "4"}, "8w": {"GCG_GEMM_8W": "1"}}
+    knobs = {"rt2": {"GCG_GEMM_RT": "2", "GCG_GEMM_OCC2": "0"},
+             "rt4": {"GCG_GEMM_RT": "4", "GCG_GEMM_OCC2": "0"},
+             "8w": {"GCG_GEMM_8W": "1"}, "occ2": {"GCG_GEMM_OCC2": "1"}}
     for name in args.tiles.split(","):  # wide-tile variants (experiment knobs of dense.hip)
         for k, v in knobs[name].items():
             os.environ[k] = v
