@@ -147,8 +147,8 @@ class Projection:
                ) -> torch.Tensor:
         return _MatMul.apply(A, W, b, self.fwd, self.bwd)
 
-    def softmax_xent(self, P, W, b, labels):
-        return _ProjectXent.apply(P, W, b, labels, self)
+    def softmax_xent(self, P, W, b, labels, denom: Optional[int] = None):
+        return _ProjectXent.apply(P, W, b, labels, self, denom)
 
     def probabilities(self, P, W, b) -> torch.Tensor:
         """softmax(P . W + b) rows (predict_proba) in one fused launch."""
@@ -194,20 +194,21 @@ class _ProjectXent(torch.autograd.Function):
     dP = G . (g W)^T, dW = g P^T . G (plain GEMMs: hipBLASLt), db = g colsum(G)."""
 
     @staticmethod
-    def forward(ctx, P, W, b, labels, proj: Projection):
+    def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None):
         P = _aligned_operand(P, "P")
         M, N = P.shape[0], W.shape[1]
+        D = float(max(M if denom is None else denom, 1))  # rows the mean is over (all ranks)
         y = _labels_i32(labels, M, N)
         need_grad = any(ctx.needs_input_grad[:3])
         G = empty_dense(M, N, P.device) if need_grad else None
         loss_rows = torch.empty(M, dtype=torch.float32, device=P.device)
         correct = torch.empty(M, dtype=torch.float32, device=P.device)
-        _fused(P, proj.fwd.get(W, False), b, y, 1.0 / max(M, 1), None, G, loss_rows, correct)
+        _fused(P, proj.fwd.get(W, False), b, y, 1.0 / D, None, G, loss_rows, correct)
         ctx.save_for_backward(P, W, G)
         ctx.proj = proj
         ctx.has_b = b is not None
-        loss = loss_rows.mean()
-        acc = correct.mean()
+        loss = loss_rows.sum() / D
+        acc = correct.sum() / D
         ctx.mark_non_differentiable(acc)
         return loss, acc
 
@@ -223,7 +224,7 @@ class _ProjectXent(torch.autograd.Function):
             gW = torch.matmul(P.t(), G).mul_(g)
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = G.sum(dim=0).mul_(g)
-        return gP, gW, gb, None, None
+        return gP, gW, gb, None, None, None
 
 
 def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct):
@@ -244,7 +245,7 @@ class _SoftmaxXent(torch.autograd.Function):
     g (softmax - onehot)/M in one more pass, g read on the device (graph-capturable)."""
 
     @staticmethod
-    def forward(ctx, logits, labels):
+    def forward(ctx, logits, labels, denom: Optional[int] = None):
         _require_cuda(logits, "logits")
         if logits.dtype != torch.float32 or logits.dim() != 2 or \
                 (logits.shape[1] > 1 and logits.stride(1) != 1):
@@ -255,9 +256,10 @@ class _SoftmaxXent(torch.autograd.Function):
         correct = torch.empty(M, dtype=torch.float32, device=logits.device)
         _rows_call(logits, y, 1.0, None, None, loss_rows, correct)
         ctx.save_for_backward(logits, y)
-        acc = correct.mean()
+        ctx.D = float(max(M if denom is None else denom, 1))
+        acc = correct.sum() / ctx.D
         ctx.mark_non_differentiable(acc)
-        return loss_rows.mean(), acc
+        return loss_rows.sum() / ctx.D, acc
 
     @staticmethod
     def backward(ctx, g_loss, _g_acc):
@@ -266,19 +268,22 @@ class _SoftmaxXent(torch.autograd.Function):
         gl = empty_dense(M, N, logits.device)
         dummy = torch.empty(M, dtype=torch.float32, device=logits.device)
         g = g_loss.reshape(1).to(torch.float32).contiguous()
-        _rows_call(logits, y, 1.0 / max(M, 1), g, gl, dummy, None)
-        return gl, None
+        _rows_call(logits, y, 1.0 / ctx.D, g, gl, dummy, None)
+        return gl, None, None
 
 
-def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None
-                         ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(mean CE loss, accuracy) of softmax(P . W + b) against labels, differentiable in P, W, b."""
-    return _ProjectXent.apply(P, W, b, labels, proj or Projection())
+def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None,
+                         denom: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mean CE loss, accuracy) of softmax(P . W + b) against labels, differentiable in P, W, b.
+    denom: the row count the mean is taken over (default: these rows; the total over all
+    ranks when each rank holds a share of the targets)."""
+    return _ProjectXent.apply(P, W, b, labels, proj or Projection(), denom)
 
 
-def softmax_xent(logits: torch.Tensor, labels: torch.Tensor) -> Tuple[torch.Tensor, torch.Tensor]:
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int] = None
+                 ) -> Tuple[torch.Tensor, torch.Tensor]:
     """(mean CE loss, accuracy) of existing logits, differentiable in the logits."""
-    return _SoftmaxXent.apply(logits, labels)
+    return _SoftmaxXent.apply(logits, labels, denom)
 
 
 def softmax(logits: torch.Tensor) -> torch.Tensor:

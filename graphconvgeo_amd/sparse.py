@@ -65,11 +65,27 @@ class RowSelection:
         return self.n
 
 
+# Plans released by the garbage collector are destroyed later, at the next plan creation (always
+# outside a HIP graph capture: creating a plan synchronizes), never inside __del__: a collection
+# can run in the middle of a capture, and hipFree there invalidates it.
+_RETIRED_PLANS: list = []
+
+
+def _destroy_retired_plans():
+    while _RETIRED_PLANS:
+        h = _RETIRED_PLANS.pop()
+        try:
+            _native.load().gcg_spmm_plan_destroy(h)
+        except Exception:  # interpreter shutdown
+            pass
+
+
 class Plan:
     """Owning wrapper of a gcg_spmm_plan (nnz-balanced task list for one CSR + rows)."""
 
     def __init__(self, A: "DeviceCSR", rows: Optional[RowSelection], ordered: bool,
                  task_nnz: int):
+        _destroy_retired_plans()
         self.A = A
         self.rows = rows
         self.ordered = bool(ordered)
@@ -102,10 +118,7 @@ class Plan:
     def __del__(self):
         h = getattr(self, "handle", None)
         if h is not None and h.value:
-            try:
-                _native.load().gcg_spmm_plan_destroy(h)
-            except Exception:  # interpreter shutdown
-                pass
+            _RETIRED_PLANS.append(h)  # destroyed at the next plan creation (see above)
             self.handle = None
 
 

@@ -117,3 +117,100 @@ def test_feature_parallel_columns_concatenate_to_full():
         fp = FeatureParallelSpMM(H, r, 3, "cpu", 30, local_spmm=_oracle_spmm)
         parts.append(fp.spmm(torch.from_numpy(np.ascontiguousarray(Z[:, fp.c0:fp.c1]))).numpy())
     assert np.array_equal(np.concatenate(parts, axis=1), ref)  # column-local: bitwise
+
+
+class _CPUOps:
+    """Test-only rank-local ops for the partitioned propagate: the CPU oracle."""
+
+    @staticmethod
+    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto"):
+        from oracle import gcn_oracle as O
+        r = None if rows is None else rows.host
+        b = None if bias is None else bias.numpy()
+        return torch.from_numpy(O.spmm_f32(A, Z.numpy(), bias=b, act=act, rows=r))
+
+    @staticmethod
+    def scatter_rows(n_rows, rows, g):
+        from oracle import gcn_oracle as O
+        out = np.zeros((n_rows, g.shape[1]), np.float32)
+        O.scatter_add_f32(out, rows.host, g.detach().numpy())
+        return torch.from_numpy(out)
+
+
+def _prop_worker(rank, world, port, n, e, K, q, exchange):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphconvgeo_amd import sparse as gs
+        from graphconvgeo_amd.dist_train import local_targets, partitioned_propagate
+        from graphconvgeo_amd.distributed import RowPartitionedCSR
+        H = synthetic_graph(n, e)
+        rng = np.random.default_rng(11)
+        Z = rng.standard_normal((n, K)).astype(np.float32)
+        b = rng.standard_normal(K).astype(np.float32)
+        targets = rng.integers(0, n, size=n // 2).astype(np.int32)  # duplicates included
+        part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm, exchange=exchange)
+        Zp = torch.from_numpy(part.local_rows(Z).copy()).requires_grad_()
+        bt = torch.from_numpy(b).requires_grad_()
+        h = partitioned_propagate(Zp, part, bt, "relu", None, ops=_CPUOps)
+        pos, loc = local_targets(targets, part.start, part.stop)
+        rows = gs.RowSelection(loc, "cpu")
+        P = partitioned_propagate(h, part, None, None, rows, ops=_CPUOps)
+        R = torch.from_numpy(rng.standard_normal((targets.size, K)).astype(np.float32))
+        (P * R[torch.from_numpy(pos)]).sum().backward()
+        out = [None] * world
+        dist.all_gather_object(out, (part.start, part.stop, pos, P.detach().numpy(),
+                                     Zp.grad.numpy(), bt.grad.numpy()))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("exchange", ["allgather", "halo"])
+def test_partitioned_propagate_fwd_bwd(exchange):
+    """Two stacked partitioned propagates (rectify, then a target-row subset with duplicates)
+    and their backward through H's symmetry: activations and input gradients bitwise equal to
+    the single-process oracle chain; the bias gradient (a cross-rank sum) within fp32."""
+    from oracle import gcn_oracle as O
+    n, e, K, world = 2500, 16000, 12, 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_prop_worker, args=(r, world, port, n, e, K, q, exchange))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    out = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    H = synthetic_graph(n, e)
+    rng = np.random.default_rng(11)
+    Z = rng.standard_normal((n, K)).astype(np.float32)
+    b = rng.standard_normal(K).astype(np.float32)
+    targets = rng.integers(0, n, size=n // 2).astype(np.int32)
+    R = rng.standard_normal((targets.size, K)).astype(np.float32)
+    h = O.spmm_f32(H, Z, bias=b, act="relu")
+    P = O.spmm_f32(H, h, rows=targets)
+    g_h = np.zeros((n, K), np.float32)
+    O.scatter_add_f32(g_h, targets, R)
+    g_h = O.spmm_f32(H, g_h)                      # H^T = H
+    g_pre = g_h * (h > 0)
+    g_Z = O.spmm_f32(H, g_pre.astype(np.float32))
+    got_P = np.zeros_like(P)
+    got_gZ = np.zeros_like(g_Z)
+    g_b = np.zeros(K, np.float64)
+    for start, stop, pos, Pp, gZp, gbp in out:
+        got_P[pos] = Pp
+        got_gZ[start:stop] = gZp
+        g_b += gbp
+    assert np.array_equal(got_P, P)
+    assert np.array_equal(got_gZ, g_Z)
+    assert np.allclose(g_b, g_pre.astype(np.float64).sum(0), rtol=1e-5, atol=1e-4)
+
+
+def test_local_targets_keeps_order_and_duplicates():
+    from graphconvgeo_amd.dist_train import local_targets
+    pos, loc = local_targets(np.array([5, 1, 7, 5, 3, 9]), 3, 8)
+    assert pos.tolist() == [0, 2, 3, 4] and loc.tolist() == [2, 4, 2, 0]

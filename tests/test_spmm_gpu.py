@@ -240,3 +240,30 @@ def test_pipelined_partition_bitwise(cuda, chunks):
     Y = gs.empty_dense(4_000, 300, cuda)
     part.spmm_pipelined(to_dev(Z, cuda), Y, n_chunks=chunks, mode="ordered")
     assert np.array_equal(Y.cpu().numpy(), O.spmm_f32(H, Z))
+
+
+def test_plan_released_during_graph_capture_is_deferred(cuda):
+    """A plan whose owner dies while a HIP graph is being captured (a GC pass can run inside
+    the capture) must not hipFree there: destruction is deferred to the next plan creation."""
+    import gc
+    import torch
+    from graphconvgeo_amd import sparse as gs
+    from graphconvgeo_amd.synth import synthetic_graph
+    H = synthetic_graph(3000, 20000)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    doomed = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    Z = torch.randn((3000, 16), device=cuda)
+    Y = gs.spmm(A, Z, mode="ordered")
+    gs.spmm(doomed, Z, mode="ordered")  # doomed now owns a plan
+    doomed._self = doomed  # reference cycle: only the cycle collector frees it
+    del doomed
+    g = torch.cuda.CUDAGraph()
+    out = torch.empty_like(Y)
+    with torch.cuda.graph(g):
+        gs.spmm(A, Z, out=out, mode="ordered")
+        gc.collect()  # the doomed operator and its plan die inside the capture
+    g.replay()
+    torch.cuda.synchronize()
+    assert torch.equal(out, Y)
+    gs.spmm(gs.DeviceCSR.from_scipy(H, cuda, symmetric=True), Z, mode="ordered")  # flushes
+    assert not gs._RETIRED_PLANS
