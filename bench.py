@@ -41,6 +41,11 @@ def spmm_bytes(n_rows: int, nnz: int, K: int) -> int:
     return 4 * (n_rows + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n_rows
 
 
+def compulsory_bytes(n_rows: int, nnz: int, K: int, n_cols: int) -> int:
+    """indptr + (idx, val) + Z read once + Y written once."""
+    return 4 * (n_rows + 1) + 8 * nnz + 4 * K * n_cols + 4 * K * n_rows
+
+
 def cpu_model() -> str:
     try:
         with open("/proc/cpuinfo") as f:
@@ -254,7 +259,12 @@ def main():
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                     "traffic": traffic, "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
-                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": kbytes}
+                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": kbytes,
+                    # compulsory bytes (every array touched once) beside the
+                    # edge-centric count, so cache reuse on the gather is visible
+                    "compulsory_bytes_per_launch": (
+                        compulsory_bytes(N, nnz, K, N) if kbytes == B else
+                        compulsory_bytes(part.n_local, part.nnz_local, K, part.operand_rows()))}
         if traffic_src:
             roofline["traffic_source"] = traffic_src
         if kbytes != B:

@@ -103,11 +103,12 @@ class _CSRMatMul(torch.autograd.Function):
         g_Z = None
         if ctx.needs_input_grad[0]:
             if rows is not None:
-                full = torch.zeros((A.n_rows, g.shape[1]), dtype=torch.float32, device=g.device)
-                seg_ptr, pos = _index_csr_cached(rows, A.n_rows)
-                gs.scatter_add_rows(full, seg_ptr, pos, g.contiguous())
-                g = full
-            g_Z = gs.spmm(A.transpose(), g.contiguous(), mode=ctx.mode)
+                # (A[rows])^T . g: one SpMM over the targets' nonzeros (sparse.rows_transpose),
+                # equal to A^T . inc_subtensor(zeros, rows, g) (mlpconv.py:94, Theano's grad)
+                # within fp32 rounding
+                g_Z = gs.spmm(A.rows_transpose(rows), g.contiguous(), mode=ctx.mode)
+            else:
+                g_Z = gs.spmm(A.transpose(), g.contiguous(), mode=ctx.mode)
         return g_Z, g_bias, None, None, None, None
 
 

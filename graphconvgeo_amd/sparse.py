@@ -225,6 +225,34 @@ class DeviceCSR:
             self._transpose = t
         return self._transpose
 
+    def rows_transpose(self, rows: RowSelection) -> "DeviceCSR":
+        """CSR of (A[rows])^T, built on the device once per row list and cached: the operator
+        of the gradient of A[rows] . Z w.r.t. Z. Row j lists, in target order, every target
+        position p whose row rows[p] holds column j -- duplicated targets stay separate entries
+        (tensormain.py:226 draws with replacement). One SpMM with it replaces the scatter-add
+        of the row gradient into an N-row zero matrix followed by a full A^T SpMM: it touches
+        sum(row lengths of the targets) nonzeros instead of nnz(A), and no N-row temporary."""
+        cache = self.__dict__.setdefault("_rows_t", {})
+        t = cache.get(rows.key)
+        if t is None:
+            idx = rows.device_rows.to(torch.int64)
+            starts = self.indptr.to(torch.int64)[idx]
+            lens = self.indptr.to(torch.int64)[idx + 1] - starts
+            indptr = torch.zeros(rows.n + 1, dtype=torch.int64, device=self.device)
+            torch.cumsum(lens, 0, out=indptr[1:])
+            nnz = int(indptr[-1])
+            if nnz >= 2**31:
+                raise ValueError("A[rows] has too many nonzeros for int32 CSR")
+            owner = torch.repeat_interleave(torch.arange(rows.n, device=self.device), lens,
+                                            output_size=nnz)
+            src = starts[owner] + torch.arange(nnz, device=self.device) - indptr[owner]
+            gathered = DeviceCSR(indptr.to(torch.int32), self.indices[src], self.data[src],
+                                 (rows.n, self.n_cols), validate=False)
+            t = gathered.transpose()  # stable: within a row of the transpose, target order
+            t._transpose = None  # do not pin the gathered copy
+            cache[rows.key] = t
+        return t
+
     def __repr__(self):
         return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 

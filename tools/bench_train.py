@@ -57,7 +57,7 @@ def main():
     clf = MLPCONV(n_epochs=0, hidden_layer_size=cfg.hidden, device=dev, seed=1, mode=args.mode,
                   order=args.order, use_graph=args.graph)
     clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H/X, no epochs
-    y_train = torch.as_tensor(Y[train].astype(np.int64), device=dev)
+    y_train = torch.as_tensor(Y[train].astype(np.int32), device=dev)
     opt = LasagneAdam(clf.params)
     clf.n_epochs = 1  # let _make_train_step capture when --graph
     step = clf._make_train_step(opt, y_train)
@@ -75,9 +75,12 @@ def main():
     # SpMMs per step: X.W1, H.Z1, H.Z2 (train rows only), H.g2, H.g1, X^T.g; the layer-2
     # products are K wide instead of C under the propagate-first order.
     width2 = K if args.order == "propagate_first" or (args.order == "auto" and C > K) else C
-    sp = (spmm_bytes(n, nnzX, K) + spmm_bytes(n, nnzH, K) + spmm_bytes(n, nnzH, width2) +
+    # The layer-2 backward runs on (H[train])^T (sparse.rows_transpose): the targets' nonzeros
+    # only, N output rows.
+    nnz_t = int(np.diff(H.indptr)[train].sum())
+    sp = (spmm_bytes(n, nnzX, K) + spmm_bytes(n, nnzH, K) + spmm_bytes(n, nnz_t, width2) +
           spmm_bytes(n, nnzH, K) + spmm_bytes(cfg.n_features, nnzX, K))
-    sp_fwd_rows = spmm_bytes(len(train), int(np.diff(H.indptr)[train].sum()), width2)
+    sp_fwd_rows = spmm_bytes(len(train), nnz_t, width2)
     total = sp + sp_fwd_rows
     rec = {"metric": "GCN 2-layer fwd+bwd+adam step", "config": cfg.name, "ms_per_step": round(ms, 3),
            "nodes": n, "nnz_H": nnzH, "nnz_X": nnzX, "F": cfg.n_features, "K": K, "C": C,
