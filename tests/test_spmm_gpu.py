@@ -267,3 +267,33 @@ def test_plan_released_during_graph_capture_is_deferred(cuda):
     assert torch.equal(out, Y)
     gs.spmm(gs.DeviceCSR.from_scipy(H, cuda, symmetric=True), Z, mode="ordered")  # flushes
     assert not gs._RETIRED_PLANS
+
+
+def test_rows_transpose_equals_scipy(cuda):
+    """(H[idx])^T built on the device: same entries, same within-row order (target order) as
+    scipy's stable `H[idx].T.tocsr()`; duplicated targets stay separate entries; the SpMM with
+    it equals the scatter-then-H^T form within fp32 rounding."""
+    import numpy as np
+    import torch
+    from graphconvgeo_amd import sparse as gs
+    from graphconvgeo_amd.synth import synthetic_graph
+    from oracle import gcn_oracle as O
+    H = synthetic_graph(5000, 40000)
+    idx = np.random.default_rng(4).integers(0, 5000, size=3000).astype(np.int32)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    rows = gs.RowSelection(idx, cuda)
+    T = A.rows_transpose(rows)
+    ref = H[idx].T.tocsr()
+    assert T.shape == ref.shape
+    assert np.array_equal(T.indptr.cpu().numpy(), ref.indptr)
+    assert np.array_equal(T.indices.cpu().numpy(), ref.indices)
+    assert np.array_equal(T.data.cpu().numpy(), ref.data)
+    assert A.rows_transpose(gs.RowSelection(idx, cuda)) is T  # cached by content
+    g = np.random.default_rng(5).standard_normal((3000, 24)).astype(np.float32)
+    got = gs.spmm(T, torch.from_numpy(g).to(cuda), mode="ordered").cpu().numpy()
+    assert np.array_equal(got, O.spmm_f32(ref, g))  # bitwise vs the oracle on the same CSR
+    full = np.zeros((5000, 24), np.float32)
+    O.scatter_add_f32(full, idx, g)
+    assert np.abs(got - O.spmm_f32(H, full)).max() < 1e-5
+    empty = A.rows_transpose(gs.RowSelection(np.zeros(0, np.int32), cuda))
+    assert empty.shape == (5000, 0) and empty.nnz == 0
