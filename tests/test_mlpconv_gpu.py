@@ -75,10 +75,14 @@ def test_mlpconv_propagate_first_order(cuda):
     assert np.abs(got - ref).max() < 1e-4 * max(1.0, np.abs(ref).max()), (got, ref)
 
 
-def test_mlpconv_hip_graph_equals_eager(cuda):
+@pytest.mark.parametrize("order", ["reference", "propagate_first"])
+def test_mlpconv_hip_graph_equals_eager(cuda, order):
+    """A captured epoch replays the eager one bit for bit; in the propagate-first order the
+    capture holds the fused MFMA output kernel and the padded-weight copy it reads (re-copied on
+    every replay, since Adam moves W2 between replays)."""
     H, X, Y, train, dev, test, init = problem(n=3000, e=20000, f=200, k=32, c=7)
     kw = dict(n_epochs=11, hidden_layer_size=32, regul_coefs=(1e-5, 1e-5), init_parameters=init,
-              device=cuda, report_k_epoch=5)
+              device=cuda, report_k_epoch=5, order=order)
     a = MLPCONV(**kw).fit(X, train, dev, test, Y, H)
     b = MLPCONV(use_graph=True, **kw).fit(X, train, dev, test, Y, H)
     assert [h["train_loss"] for h in a.history] == [h["train_loss"] for h in b.history]
