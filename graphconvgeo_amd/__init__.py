@@ -3,7 +3,9 @@
 Product modules (all compute runs in libgcg_spmm.so HIP kernels; no CPU fallback):
   sparse       DeviceCSR (H / X resident in HBM), spmm (= S.dot + fused epilogue)
   layers       GraphConvLayer, SparseConvolutionDenseLayer, ConvolutionDenseLayer, GCN
-  distributed  1-D row partition of H + RCCL all-gather of the dense operand
+  dense        output layer on the MFMA cores: f32 GEMMs, fused projection + softmax + CE
+  distributed  1-D row partition of H + RCCL all-gather / halo exchange of the dense operand
+  dist_train   the row-partitioned GCN training step (backward through H's symmetry)
   graph        H = D^-1/2 (A+I) D^-1/2 construction, host (scipy) and device (HIP)
   mentions     mention-graph parsing (host) and projection (HIP), data.py:226-375
   mlpconv      MLPCONV trainer (mlpconv.py:121-352) on the GPU
@@ -11,4 +13,5 @@ Product modules (all compute runs in libgcg_spmm.so HIP kernels; no CPU fallback
 """
 __version__ = "0.1.0"
 
-__all__ = ["sparse", "layers", "distributed", "graph", "mentions", "mlpconv", "synth"]
+__all__ = ["sparse", "layers", "dense", "distributed", "dist_train", "graph", "mentions",
+           "mlpconv", "synth"]

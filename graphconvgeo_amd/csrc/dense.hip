@@ -28,6 +28,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdio>
 #include <limits>
 
 #include "common.h"
@@ -466,6 +467,159 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
+// C = scale * A^T . B, the weight gradients h^T . g / P^T . G (Theano's grad of T.dot(h, W)
+// w.r.t. W, mlpconv.py:88): reduction over R ~ 10^6 rows into a small M x N output.
+// Split-K: blockIdx.z owns rows [z*rows_per_split, ...); each wave keeps a 64*MG x 64*NG
+// accumulator tile. Lane (j, q) loads ONE dwordx4 of A's row t and one of B's row t per
+// 64-wide group (t = t0 + q): element e of the A vector is row-slot j of the MFMA tile that
+// owns the C rows m0 + 4j + e, element e' of the B vector the column-slot j of the tile owning
+// the C columns n0 + 4j + e' -- so 2 loads feed 16 v_mfma_f32_16x16x4_f32 and a lane's
+// accumulators hold 4 adjacent C columns (dwordx4 partial stores). A ring of PD register
+// sets keeps PD steps of loads in flight. Partials [split][Mp][Np] are summed in split order
+// by gemm_tn_reduce_kernel (deterministic), which applies scale (a device scalar).
+// ---------------------------------------------------------------------------------------
+template <int MG, int NG, int PD>
+__global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
+    int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+    int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, q = lane >> 4;
+  const int m0 = blockIdx.x * (64 * MG);
+  const int n0 = blockIdx.y * (256 * NG) + wave * (64 * NG);
+  const int t_begin = blockIdx.z * rows_per_split;
+  const int t_end = min(R, t_begin + rows_per_split);
+  const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
+  int acol[MG], bcol[NG];
+#pragma unroll
+  for (int g = 0; g < MG; ++g) {
+    const int c = m0 + 64 * g + 4 * j;
+    acol[g] = c < m4 ? c : 0;  // rows of C past M: computed on a valid column, never stored
+  }
+#pragma unroll
+  for (int g = 0; g < NG; ++g) {
+    const int c = n0 + 64 * g + 4 * j;
+    bcol[g] = c < n4 ? c : 0;
+  }
+  f4 acc[MG][NG][4][4];
+#pragma unroll
+  for (int a = 0; a < MG; ++a)
+#pragma unroll
+    for (int b = 0; b < NG; ++b)
+#pragma unroll
+      for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+        for (int eb = 0; eb < 4; ++eb) acc[a][b][ea][eb] = f4{0.f, 0.f, 0.f, 0.f};
+
+  f4 ra[PD][MG], rb[PD][NG];
+  auto load = [&](int u, int t0) {
+    const int t = t0 + q;
+    const bool ok = t < t_end;
+    const int tc = ok ? t : t_begin;  // clamped row, zeroed below
+    const float* arow = A + static_cast<int64_t>(tc) * lda;
+    const float* brow = B + static_cast<int64_t>(tc) * ldb;
+#pragma unroll
+    for (int g = 0; g < MG; ++g) {
+      f4 v = *reinterpret_cast<const f4*>(arow + acol[g]);
+      ra[u][g] = ok ? v : f4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int g = 0; g < NG; ++g) rb[u][g] = *reinterpret_cast<const f4*>(brow + bcol[g]);
+  };
+  auto compute = [&](int u) {
+#pragma unroll
+    for (int a = 0; a < MG; ++a)
+#pragma unroll
+      for (int b = 0; b < NG; ++b)
+#pragma unroll
+        for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+          for (int eb = 0; eb < 4; ++eb)
+            acc[a][b][ea][eb] = mfma4(ra[u][a][ea], rb[u][b][eb], acc[a][b][ea][eb]);
+  };
+  // steps of 4 rows; the ring is refilled PD steps ahead (loads past t_end are zeroed)
+#pragma unroll
+  for (int u = 0; u < PD; ++u) load(u, t_begin + 4 * u);
+  for (int t0 = t_begin; t0 < t_end; t0 += 4 * PD) {
+#pragma unroll
+    for (int u = 0; u < PD; ++u) {
+      compute(u);
+      load(u, t0 + 4 * (u + PD));
+    }
+  }
+  // partial tile: lane holds C[m0 + 64a + 16q + 4r + ea][n0 + 64b + 4j + eb] in acc[a][b][ea][eb][r]
+  float* dst = part + static_cast<int64_t>(blockIdx.z) * Mp * Np;
+#pragma unroll
+  for (int a = 0; a < MG; ++a)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int ea = 0; ea < 4; ++ea) {
+        const int m = m0 + 64 * a + 16 * q + 4 * r + ea;
+        float* row = dst + static_cast<int64_t>(m) * Np;
+#pragma unroll
+        for (int b = 0; b < NG; ++b) {
+          const int n = n0 + 64 * b + 4 * j;
+          *reinterpret_cast<f4*>(row + n) = f4{acc[a][b][ea][0][r], acc[a][b][ea][1][r],
+                                               acc[a][b][ea][2][r], acc[a][b][ea][3][r]};
+        }
+      }
+}
+
+// C[m][n] = scale * sum_{s in order} part[s][m][n]; one thread per (m, 4 columns).
+__global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
+    int M, int N, int S, const float* __restrict__ part, int Mp, int Np,
+    const float* __restrict__ scale_dev, float* __restrict__ C, int64_t ldc, int vec) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  const int nq = (N + 3) / 4;
+  if (i >= static_cast<int64_t>(M) * nq) return;
+  const int m = static_cast<int>(i / nq), n = static_cast<int>(i % nq) * 4;
+  const float* src = part + static_cast<int64_t>(m) * Np + n;
+  f4 acc = *reinterpret_cast<const f4*>(src);
+  for (int s = 1; s < S; ++s) {
+    const f4 v = *reinterpret_cast<const f4*>(src + static_cast<int64_t>(s) * Mp * Np);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  const float sc = scale_dev ? *scale_dev : 1.0f;
+  float* crow = C + static_cast<int64_t>(m) * ldc;
+  const f4 o = {acc.x * sc, acc.y * sc, acc.z * sc, acc.w * sc};
+  if (vec && n + 3 < N) {
+    *reinterpret_cast<f4*>(crow + n) = o;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      if (n + e < N) crow[n + e] = o[e];
+  }
+}
+
+struct TnPlan {
+  int mg, ng, pd;  // tile variant
+  int mt, nt, S, rows_per_split, Mp, Np;
+};
+
+TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
+  TnPlan p;
+  p.mg = 1, p.ng = 2, p.pd = 8;
+  if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD"
+    int a = 0, b = 0, c = 0;
+    if (std::sscanf(v, "%d,%d,%d", &a, &b, &c) == 3) p.mg = a, p.ng = b, p.pd = c;
+  }
+  p.mt = static_cast<int>((M + 64 * p.mg - 1) / (64 * p.mg));
+  p.nt = static_cast<int>((N + 256 * p.ng - 1) / (256 * p.ng));
+  // ~2 workgroups per CU-slot of the 256 CUs, at least 256 rows per split, 16-row aligned
+  const int64_t want = std::max<int64_t>(1, 2048 / std::max(1, p.mt * p.nt));
+  const int64_t max_s = std::max<int64_t>(1, R / 256);
+  p.S = static_cast<int>(std::min(want, max_s));
+  int64_t rps = (R + p.S - 1) / p.S;
+  rps = (rps + 15) / 16 * 16;
+  p.rows_per_split = static_cast<int>(std::max<int64_t>(rps, 16));
+  p.S = static_cast<int>((R + p.rows_per_split - 1) / p.rows_per_split);
+  p.Mp = p.mt * 64 * p.mg;
+  p.Np = p.nt * 256 * p.ng;
+  return p;
+}
+
+// ---------------------------------------------------------------------------------------
 // Host side
 // ---------------------------------------------------------------------------------------
 
@@ -640,6 +794,66 @@ gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64
   GCG_SX_CASE(16)
 #undef GCG_SX_CASE
   return fail(GCG_ERR_INVALID_ARG, "%s: N too large", fn);
+}
+
+gcg_status gcg_gemm_tn_f32_workspace_bytes(int64_t R, int64_t M, int64_t N, size_t* bytes) {
+  if (R < 0 || M <= 0 || N <= 0 || R > INT32_MAX || M > INT32_MAX || N > INT32_MAX ||
+      bytes == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_tn_f32_workspace_bytes: bad sizes");
+  if (R == 0) { *bytes = 0; return GCG_OK; }
+  const TnPlan p = tn_plan(R, M, N);
+  *bytes = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
+  return GCG_OK;
+}
+
+gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
+                           const float* B, int64_t ldb, const float* scale_dev, float* C,
+                           int64_t ldc, void* workspace, size_t workspace_bytes,
+                           gcg_stream_t stream) {
+  const char* fn = "gcg_gemm_tn_f32";
+  if (R < 0 || M <= 0 || N <= 0 || R > INT32_MAX || M > INT32_MAX || N > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes R=%lld M=%lld N=%lld", fn,
+                static_cast<long long>(R), static_cast<long long>(M), static_cast<long long>(N));
+  gcg_status st;
+  // dwordx4 row reads at columns < round4(M) / round4(N)
+  if ((st = check_dense(fn, A, lda, (M + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
+  if ((st = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
+  if ((st = check_dense(fn, C, ldc, N, false)) != GCG_OK) return st;
+  auto s = static_cast<hipStream_t>(stream);
+  if (R == 0) {
+    for (int64_t m = 0; m < M; ++m)
+      GCG_HIP_CHECK(hipMemsetAsync(C + m * ldc, 0, sizeof(float) * N, s));
+    return GCG_OK;
+  }
+  const TnPlan p = tn_plan(R, M, N);
+  const size_t need = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
+  if (workspace == nullptr || workspace_bytes < need)
+    return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu bytes < %zu needed", fn, workspace_bytes,
+                need);
+  if (!aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace not 16-B aligned", fn);
+  float* part = static_cast<float*>(workspace);
+  const dim3 grid(p.mt, p.nt, p.S);
+#define GCG_TN_CASE(MG_, NG_, PD_)                                                           \
+  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_) {                                           \
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_>), grid, dim3(256), 0, s, int(R),\
+                       int(M), int(N), A, lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np);  \
+  } else
+  GCG_TN_CASE(1, 2, 4)
+  GCG_TN_CASE(1, 2, 8)
+  GCG_TN_CASE(1, 1, 8)
+  GCG_TN_CASE(1, 2, 12)
+  GCG_TN_CASE(1, 2, 16)
+  GCG_TN_CASE(1, 1, 16)
+  { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
+#undef GCG_TN_CASE
+  GCG_HIP_CHECK(hipGetLastError());
+  const int64_t threads = M * ((N + 3) / 4);
+  const int vec = (ldc % 4 == 0 && aligned(C, 16)) ? 1 : 0;
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)),
+                     dim3(256), 0, s, int(M), int(N), p.S, part, p.Mp, p.Np, scale_dev, C, ldc,
+                     vec);
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
 }
 
 }  // extern "C"

@@ -14,13 +14,16 @@ Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
                                   (softmax - onehot)/T is produced in the same pass
   softmax_xent(logits, y)         loss, acc of logits that already exist (reference order)
   softmax(logits)                 predict_proba
-The weight-gradient reduction over rows (h^T . g, K x C) stays a library GEMM (torch.matmul
--> hipBLASLt): it is a plain tall-skinny GEMM with nothing to fuse.
+  gemm_tn(A, B)                   C = A^T . B, the weight gradient h^T . g: a split-K MFMA kernel
+                                  (reduction over ~10^6 rows), deterministic
+The plain forward / input-gradient GEMMs stay on hipBLASLt, measured faster on these shapes.
 There is no CPU path: CPU tensors raise.
 """
 from __future__ import annotations
 
 from typing import Optional, Tuple
+
+import ctypes as C
 
 import torch
 
@@ -110,16 +113,57 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
     return out
 
 
+_TN_WS: dict = {}
+
+
+def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = scale * A^T . B (the weight gradient h^T . g) on the split-K MFMA kernel;
+    deterministic (partials summed in a fixed order). scale: optional device scalar."""
+    A = _aligned_operand(A, "A")
+    B = _aligned_operand(B, "B")
+    R, M = A.shape
+    if B.shape[0] != R:
+        raise ValueError(f"shape mismatch: A is {tuple(A.shape)}, B is {tuple(B.shape)}")
+    N = B.shape[1]
+    for t, n, cols in ((A, "A", M), (B, "B", N)):
+        if R > 1 and _ld(t) < (cols + 3) // 4 * 4:
+            t2 = empty_dense(R, cols, t.device)  # row stride must cover round4(cols)
+            t2.copy_(t)
+            if n == "A":
+                A = t2
+            else:
+                B = t2
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=A.device)
+    if R == 0:
+        return out.zero_()
+    nb = C.c_size_t()
+    call("gcg_gemm_tn_f32_workspace_bytes", R, M, N, C.byref(nb))
+    key = (A.device, torch.cuda.current_stream(A.device).cuda_stream)
+    ws = _TN_WS.get(key)
+    if ws is None or ws.numel() * 4 < nb.value:
+        ws = torch.empty(max((nb.value + 15) // 16 * 4, 4), dtype=torch.float32, device=A.device)
+        _TN_WS[key] = ws
+    if scale is not None:
+        scale = scale.reshape(1).to(torch.float32).contiguous()
+    with torch.cuda.device(A.device):
+        call("gcg_gemm_tn_f32", R, M, N, _ptr(A), _ld(A), _ptr(B), _ld(B), _ptr(scale),
+             _ptr(out), out.stride(0) if M > 1 else N, _ptr(ws), ws.numel() * 4,
+             _stream_handle(A.device))
+    return out
+
+
 class _MatMul(torch.autograd.Function):
-    """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88) and dA = g . W^T on the MFMA GEMM kernel,
-    dW = A^T . g, db = colsum(g). (The trainer's plain GEMMs use hipBLASLt, measured faster
-    on its shapes; this path serves callers that want every product in libgcg_spmm.)"""
+    """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88) and its gradients. Forward and dA = g . W^T
+    are plain GEMMs (hipBLASLt, measured faster on these shapes); the weight gradient
+    dW = A^T . g -- a reduction over ~10^6 rows into K x C -- runs on the split-K MFMA kernel
+    (gemm_tn, 1.13-1.28x hipBLASLt at Twitter-World shapes)."""
 
     @staticmethod
-    def forward(ctx, A, W, b, cache_fwd: _WeightCache, cache_bwd: _WeightCache):
-        C = gemm(A, cache_fwd.get(W, transpose=False), bias=None if b is None else b.detach())
+    def forward(ctx, A, W, b):
+        C = torch.matmul(A, W) if b is None else torch.addmm(b, A, W)
         ctx.save_for_backward(A, W)
-        ctx.cache_bwd = cache_bwd
         ctx.has_b = b is not None
         return C
 
@@ -128,12 +172,17 @@ class _MatMul(torch.autograd.Function):
         A, W = ctx.saved_tensors
         gA = gW = gb = None
         if ctx.needs_input_grad[0]:
-            gA = gemm(g, ctx.cache_bwd.get(W, transpose=True))
+            gA = torch.matmul(g, W.t())
         if ctx.needs_input_grad[1]:
-            gW = torch.matmul(A.t(), g)
+            gW = gemm_tn(A, g)
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = g.sum(dim=0)
-        return gA, gW, gb, None, None
+        return gA, gW, gb
+
+
+def matmul(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Differentiable A . W (+ b) with the weight gradient on the split-K MFMA kernel."""
+    return _MatMul.apply(A, W, b)
 
 
 class Projection:
@@ -145,9 +194,18 @@ class Projection:
 
     def matmul(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None
                ) -> torch.Tensor:
-        return _MatMul.apply(A, W, b, self.fwd, self.bwd)
+        return matmul(A, W, b)
 
     def softmax_xent(self, P, W, b, labels, denom: Optional[int] = None):
+        if not torch.is_grad_enabled():  # evaluation: loss and hits only, no gradient buffer
+            P = _aligned_operand(P, "P")
+            M = P.shape[0]
+            D = float(max(M if denom is None else denom, 1))
+            y = _labels_i32(labels, M, W.shape[1])
+            loss_rows = torch.empty(M, dtype=torch.float32, device=P.device)
+            correct = torch.empty(M, dtype=torch.float32, device=P.device)
+            _fused(P, self.fwd.get(W, False), b, y, 1.0, None, None, loss_rows, correct)
+            return loss_rows.sum() / D, correct.sum() / D
         return _ProjectXent.apply(P, W, b, labels, self, denom)
 
     def probabilities(self, P, W, b) -> torch.Tensor:
@@ -191,7 +249,7 @@ class _ProjectXent(torch.autograd.Function):
 
     Forward: one fused MFMA launch writes G = (softmax - onehot)/M (the logits gradient),
     per-row losses and hits; no logits in HBM. Backward (upstream g, a device scalar):
-    dP = G . (g W)^T, dW = g P^T . G (plain GEMMs: hipBLASLt), db = g colsum(G)."""
+    dP = G . (g W)^T (hipBLASLt), dW = g P^T . G (split-K MFMA gemm_tn), db = g colsum(G)."""
 
     @staticmethod
     def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None):
@@ -221,7 +279,7 @@ class _ProjectXent(torch.autograd.Function):
             # plain GEMM: hipBLASLt measured faster here (4.3 vs 5.2 ms at 840k x 930 x 300)
             gP = torch.matmul(G, (W.detach() * g).t())
         if ctx.needs_input_grad[1]:
-            gW = torch.matmul(P.t(), G).mul_(g)
+            gW = gemm_tn(P, G, scale=g)  # split-K MFMA, the upstream gradient applied on device
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = G.sum(dim=0).mul_(g)
         return gP, gW, gb, None, None, None

@@ -157,7 +157,7 @@ class RowPartitionedGCN:
             P = partitioned_propagate(h, self.part, None, None, self.rows, self.mode)
             loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, self.y_p, denom=self.T_total)
         else:
-            Z2 = torch.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
+            Z2 = dense.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
             logits = partitioned_propagate(Z2, self.part, self.b2, None, self.rows, self.mode)
             loss, acc = dense.softmax_xent(logits, self.y_p, denom=self.T_total)
         if self.rank == 0:

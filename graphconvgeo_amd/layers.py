@@ -11,8 +11,9 @@ Reference (Lasagne `Layer` subclasses, Theano graph, host CPU):
 Here: torch modules with the same constructor arguments and `get_output_for` /
 `forward(input, target_indices=None)`. The sparse products run in the HIP kernels
 (graphconvgeo_amd.sparse.spmm) with bias + rectify + the target-row subset fused in the
-epilogue; the dense projection T.dot(h, W) is a plain fp32 GEMM (torch.matmul ->
-hipBLASLt/rocBLAS on the f32 MFMA path). Backward follows Theano's rules: grad of
+epilogue; the dense projection T.dot(h, W) is an fp32 GEMM on the f32 MFMA path (hipBLASLt
+forward, its weight gradient on the split-K MFMA kernel of csrc/dense.hip; the trainer's
+output layer is one fused MFMA kernel, graphconvgeo_amd.dense). Backward follows Theano's rules: grad of
 S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H for the symmetric H; CSR(X^T) built once on the
 device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
 
@@ -29,6 +30,7 @@ import scipy.sparse as sps
 import torch
 import torch.nn as nn
 
+from . import dense
 from . import sparse as gs
 
 _FUSED_ACTS = {"rectify": "relu", "relu": "relu"}
@@ -189,7 +191,7 @@ class GraphConvLayer(nn.Module):
         if is_sparse:
             Z = csr_matmul(self._sparse_input(input), self.W, mode=self.mode)  # S.dot(X, W)
         else:
-            Z = torch.matmul(input, self.W)  # T.dot(h, W), mlpconv.py:88
+            Z = dense.matmul(input, self.W)  # T.dot(h, W), mlpconv.py:88 (dW: split-K MFMA)
         rows = None
         if target_indices is not None:
             rows = target_indices if isinstance(target_indices, gs.RowSelection) else \
@@ -247,7 +249,7 @@ class ConvolutionDenseLayer(GraphConvLayer):
         if self.order == "reference" or isinstance(input, gs.DeviceCSR) or sps.issparse(input):
             return super().forward(input, target_indices=target_indices, **kwargs)
         P = self.propagate(input, target_indices)  # (H . h)[rows], K wide
-        Y = torch.addmm(self.b, P, self.W) if self.b is not None else P @ self.W
+        Y = dense.matmul(P, self.W, self.b)
         if self.fused_act == "relu":
             Y = torch.relu(Y)
         return self.post(Y) if self.post is not None else Y

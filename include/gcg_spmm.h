@@ -260,6 +260,20 @@ gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64
                                 int64_t ldo, float* loss_rows, float* correct_rows /*nullable*/,
                                 gcg_stream_t stream);
 
+/*
+ * Weight gradient C = scale * A^T . B (Theano's grad of T.dot(h, W) w.r.t. W: h^T . gz,
+ * mlpconv.py:88; P^T . G in the propagate-first order), A: R x M, B: R x N, C: M x N, the
+ * reduction over R (~10^6 rows) split across workgroups on the f32 MFMA path; the per-split
+ * partials (caller-owned workspace, size from _workspace_bytes) are summed in split order, so
+ * the result is deterministic (equal to a BLAS sgemm within f32 rounding). A and B: 16-B aligned,
+ * lda >= round4(M), ldb >= round4(N), ld % 4 == 0. scale_dev: nullable device scalar.
+ */
+gcg_status gcg_gemm_tn_f32_workspace_bytes(int64_t R, int64_t M, int64_t N, size_t* bytes);
+gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
+                           const float* B, int64_t ldb, const float* scale_dev /*nullable*/,
+                           float* C, int64_t ldc, void* workspace, size_t workspace_bytes,
+                           gcg_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

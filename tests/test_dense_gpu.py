@@ -169,3 +169,27 @@ def test_fused_rejects_too_many_classes(cuda):
     with pytest.raises(ValueError):
         dense.project_softmax_xent(torch.randn(4, 8, device=cuda), torch.randn(8, 1025, device=cuda),
                                    None, torch.zeros(4, dtype=torch.int64, device=cuda))
+
+
+@pytest.mark.parametrize("R,M,N", [(1, 1, 1), (7, 3, 5), (100, 64, 129), (4097, 300, 930),
+                                   (20000, 48, 60), (3, 320, 1024), (0, 4, 4)])
+def test_gemm_tn_vs_float64(cuda, R, M, N):
+    """Weight-gradient GEMM C = A^T . B (split-K MFMA, partials summed in split order)."""
+    A, B = _rand((R, M), 41, 0.5), _rand((R, N), 42, 0.5)
+    At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
+    C = dense.gemm_tn(At, Bt).cpu().numpy()
+    _check_gemm(C, A.T.copy(), B)
+    C2 = dense.gemm_tn(At, Bt).cpu().numpy()
+    assert np.array_equal(C, C2)  # deterministic
+    sc = torch.tensor(2.5, device=cuda)
+    C3 = dense.gemm_tn(At, Bt, scale=sc).cpu().numpy()
+    assert np.array_equal(C3, (C * np.float32(2.5)))
+
+
+def test_gemm_tn_strided_views(cuda):
+    R, M, N = 3000, 300, 930
+    A, B = _rand((R, M), 43), _rand((R, N), 44)
+    Bbuf = empty_dense(R, N, cuda)  # ld 932, the layout of the fused kernel's gradient
+    Bbuf.copy_(torch.from_numpy(B))
+    C = dense.gemm_tn(torch.from_numpy(A).to(cuda), Bbuf).cpu().numpy()
+    _check_gemm(C, A.T.copy(), B)

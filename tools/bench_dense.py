@@ -50,6 +50,7 @@ def main():
     ap.add_argument("--classes", type=int, default=930)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", default="rt2,rt4,8w,occ2", help="wide-tile variants to compare")
+    ap.add_argument("--tn", default="1:2:8,1:2:12,1:2:16,1:1:16", help="TN tile variants")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     T, N, K, C = args.rows, args.nodes, args.hidden, args.classes
@@ -114,12 +115,19 @@ def main():
     Gc = G
     rec("dP = G.W2^T", time_op(lambda: dense.gemm(Gc, Wt), args.reps), f,
         time_op(lambda: torch.matmul(Gc, W.t()), args.reps))
-    rec("dW2 = P^T.G (torch)", time_op(lambda: torch.matmul(P.t(), Gc), args.reps), f)
+    for tn in args.tn.split(","):  # split-K TN tile variants (GCG_TN=MG,NG,PD)
+        os.environ["GCG_TN"] = tn.replace(":", ",")
+        rec(f"dW2 = P^T.G tn={tn}", time_op(lambda: dense.gemm_tn(P, Gc), args.reps), f)
+    os.environ.pop("GCG_TN", None)
+    rec("dW2 = P^T.G", time_op(lambda: dense.gemm_tn(P, Gc), args.reps), f,
+        time_op(lambda: torch.matmul(P.t(), Gc), args.reps))
     del G, Gc, out
     h = empty_dense(N, K, dev).copy_(torch.rand((N, K), generator=g, device=dev))
     Z2 = empty_dense(N, C, dev)
     rec("Z2 = h.W2", time_op(lambda: dense.gemm(h, Wp, out=Z2), args.reps), 2.0 * N * K * C,
         time_op(lambda: torch.matmul(h, W), args.reps))
+    rec("dW2 = h^T.dZ2 (reference order)", time_op(lambda: dense.gemm_tn(h, Z2), args.reps),
+        2.0 * N * K * C, time_op(lambda: torch.matmul(h.t(), Z2), args.reps))
     del h, Z2
     logits = empty_dense(T, C, dev).copy_(torch.randn((T, C), generator=g, device=dev))
     gl = empty_dense(T, C, dev)
