@@ -189,3 +189,21 @@ def test_dense_abi_argument_validation_without_gpu(native_lib):
     assert rows(4, 8, a16, 8, None, 1.0, None, None, 8, None, None, None) == st["inval"]
     assert rows(4, 8, a16, 4, lab, 1.0, None, None, 8, loss, None, None) == st["inval"]  # ldl < N
     assert "gcg_softmax_xent_f32" in lib.gcg_last_error().decode()
+
+
+def test_gemm_tn_abi_without_gpu(native_lib):
+    """Split-K weight-gradient GEMM: workspace sizing and argument checks run on the host."""
+    import ctypes as C
+    lib = native_lib
+    nb = C.c_size_t()
+    assert lib.gcg_gemm_tn_f32_workspace_bytes(840_000, 300, 930, C.byref(nb)) == 0
+    # partials: splits x round64(M) x round512(N) floats, ~2 workgroups per CU
+    assert nb.value % (4 * 320 * 1024) == 0 and 100 <= nb.value // (4 * 320 * 1024) <= 2048
+    assert lib.gcg_gemm_tn_f32_workspace_bytes(0, 3, 5, C.byref(nb)) == 0 and nb.value == 0
+    assert lib.gcg_gemm_tn_f32_workspace_bytes(-1, 3, 5, C.byref(nb)) == 1
+    a16, b16, c16 = C.c_void_p(0x10000), C.c_void_p(0x20000), C.c_void_p(0x30000)
+    tn = lib.gcg_gemm_tn_f32
+    assert tn(8, 3, 5, a16, 4, b16, 8, None, c16, 5, None, 0, None) == 6      # no workspace
+    assert tn(8, 3, 5, a16, 3, b16, 8, None, c16, 5, None, 0, None) == 1      # lda < round4(M)
+    assert tn(8, 3, 5, C.c_void_p(0x10008), 4, b16, 8, None, c16, 5, None, 0, None) == 2
+    assert tn(8, 3, 5, a16, 4, b16, 8, None, c16, 4, None, 0, None) == 1      # ldc < N
