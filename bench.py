@@ -119,7 +119,7 @@ def cpu_multicore(H, K: int, budget_s: float) -> dict:
 
 def load_traffic(workload: str, per_launch_bytes: int):
     """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload."""
-    path = os.path.join(ROOT, "profiles", f"pmc_{workload}.json")
+    path = os.path.join(ROOT, "profiles", "r01", f"pmc_{workload}.json")
     if not os.path.exists(path):
         return None, None
     try:
