@@ -91,6 +91,83 @@ gcg_status sort_pairs_ws(int64_t n, int end_bit, size_t* temp_bytes) {
 
 
 
+
+// Rectify backward + bias gradient in one pass (Theano's grad of
+// rectify(S.dot(H, Z) + b), mlpconv.py:75-77): g = gY where Y > 0 else 0, written to g_out
+// (may alias gY), and per-block column partial sums of g. Block = 4 waves; wave w takes rows
+// r0 + w, r0 + w + 4, ...; lanes span the columns in dwordx4 (or dword) pieces.
+constexpr int kReluRows = 512;  // rows per block
+constexpr int kReluMaxK4 = 4;   // dwordx4 column pieces per lane (K <= 1024 on the vector path)
+
+template <int VEC>
+__global__ __launch_bounds__(256) void relu_backward_kernel(
+    int64_t M, int K, const float* gY, int64_t ldg, const float* __restrict__ Y, int64_t ldy,
+    float* g_out, int64_t ldo, float* __restrict__ partial) {
+  __shared__ float red[4][kReluMaxK4 * 64 * 4];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kReluRows;
+  const int64_t r1 = min(M, r0 + kReluRows);
+  const int pieces = (K + 64 * VEC - 1) / (64 * VEC);
+  float acc[kReluMaxK4][VEC];
+#pragma unroll
+  for (int p = 0; p < kReluMaxK4; ++p)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) acc[p][e] = 0.f;
+  for (int64_t r = r0 + w; r < r1; r += 4) {
+    const float* gr = gY + r * ldg;
+    const float* yr = Y + r * ldy;
+    float* orow = g_out + r * ldo;
+#pragma unroll
+    for (int p = 0; p < kReluMaxK4; ++p) {
+      if (p >= pieces) break;
+      const int c = (p * 64 + lane) * VEC;
+      if (c >= K) continue;
+      if constexpr (VEC == 4) {
+        if (c + 4 > K) {  // ragged tail: element-wise, never touches columns >= K
+          for (int e = 0; e < 4; ++e)
+            if (c + e < K) {
+              const float o = yr[c + e] > 0.f ? gr[c + e] : 0.f;
+              orow[c + e] = o;
+              acc[p][e] += o;
+            }
+          continue;
+        }
+        const float4 gv = *reinterpret_cast<const float4*>(gr + c);
+        const float4 yv = *reinterpret_cast<const float4*>(yr + c);
+        const float4 o = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f,
+                                     yv.z > 0.f ? gv.z : 0.f, yv.w > 0.f ? gv.w : 0.f);
+        *reinterpret_cast<float4*>(orow + c) = o;
+        acc[p][0] += o.x; acc[p][1] += o.y; acc[p][2] += o.z; acc[p][3] += o.w;
+      } else {
+        const float o = yr[c] > 0.f ? gr[c] : 0.f;
+        orow[c] = o;
+        acc[p][0] += o;
+      }
+    }
+  }
+  // combine the 4 waves (fixed order), one partial row per block
+#pragma unroll
+  for (int p = 0; p < kReluMaxK4; ++p)
+#pragma unroll
+    for (int e = 0; e < VEC; ++e) red[w][(p * 64 + lane) * VEC + e] = acc[p][e];
+  __syncthreads();
+  for (int c = threadIdx.x; c < K; c += 256) {
+    const float v = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+    partial[static_cast<int64_t>(blockIdx.x) * K + c] = v;
+  }
+}
+
+// bias_grad[c] = sum over blocks (in order) of partial[b][c]
+__global__ __launch_bounds__(256) void column_sum_kernel(int64_t n_blocks, int K,
+                                                         const float* __restrict__ partial,
+                                                         float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= K) return;
+  float s = 0.f;
+  for (int64_t b = 0; b < n_blocks; ++b) s += partial[b * K + c];
+  out[c] = s;
+}
+
 }  // namespace
 
 extern "C" {
@@ -200,5 +277,57 @@ gcg_status gcg_csr_transpose_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
   return GCG_OK;
 }
 
+
+gcg_status gcg_relu_backward_f32_workspace_bytes(int64_t M, int64_t K, size_t* bytes) {
+  if (M < 0 || K < 0 || bytes == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "gcg_relu_backward_f32_workspace_bytes: bad args");
+  *bytes = sizeof(float) * static_cast<size_t>((M + kReluRows - 1) / kReluRows) * K;
+  return GCG_OK;
+}
+
+gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
+                                 const float* Y, int64_t ldy, float* g_out, int64_t ldo,
+                                 float* bias_grad, void* workspace, size_t workspace_bytes,
+                                 gcg_stream_t stream) {
+  const char* fn = "gcg_relu_backward_f32";
+  if (M < 0 || K < 0 || K > 64 * 4 * kReluMaxK4)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld K=%lld (K <= %d)", fn,
+                static_cast<long long>(M), static_cast<long long>(K), 64 * 4 * kReluMaxK4);
+  if (M == 0 || K == 0) {
+    if (bias_grad != nullptr && K > 0)
+      GCG_HIP_CHECK(hipMemsetAsync(bias_grad, 0, sizeof(float) * K, static_cast<hipStream_t>(stream)));
+    return GCG_OK;
+  }
+  if (gY == nullptr || Y == nullptr || g_out == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "%s: null operand", fn);
+  if (ldg < K || ldy < K || ldo < K) return fail(GCG_ERR_INVALID_ARG, "%s: ld < K", fn);
+  if (!aligned(gY, 4) || !aligned(Y, 4) || !aligned(g_out, 4))
+    return fail(GCG_ERR_MISALIGNED, "%s: operand not 4-B aligned", fn);
+  const int64_t n_blocks = (M + kReluRows - 1) / kReluRows;
+  const size_t need = sizeof(float) * static_cast<size_t>(n_blocks) * K;
+  if (workspace == nullptr || workspace_bytes < need)  // the kernel always writes partials
+    return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu < %zu bytes", fn, workspace_bytes, need);
+  if (!aligned(workspace, 4)) return fail(GCG_ERR_MISALIGNED, "%s: workspace alignment", fn);
+  float* part = static_cast<float*>(workspace);
+  auto st = static_cast<hipStream_t>(stream);
+  const bool vec = ldg % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0 &&
+                   aligned(gY, 16) && aligned(Y, 16) && aligned(g_out, 16);
+  if (!vec && K > 64 * kReluMaxK4)
+    return fail(GCG_ERR_MISALIGNED, "%s: K > %d needs 16-B rows (ld %% 4 == 0)", fn,
+                64 * kReluMaxK4);
+  if (vec)
+    hipLaunchKernelGGL(relu_backward_kernel<4>, dim3(static_cast<unsigned>(n_blocks)), dim3(256),
+                       0, st, M, int(K), gY, ldg, Y, ldy, g_out, ldo, part);
+  else
+    hipLaunchKernelGGL(relu_backward_kernel<1>, dim3(static_cast<unsigned>(n_blocks)), dim3(256),
+                       0, st, M, int(K), gY, ldg, Y, ldy, g_out, ldo, part);
+  GCG_HIP_CHECK(hipGetLastError());
+  if (bias_grad != nullptr) {
+    hipLaunchKernelGGL(column_sum_kernel, dim3(static_cast<unsigned>((K + 255) / 256)), dim3(256),
+                       0, st, n_blocks, int(K), part, bias_grad);
+    GCG_HIP_CHECK(hipGetLastError());
+  }
+  return GCG_OK;
+}
 
 }  // extern "C"

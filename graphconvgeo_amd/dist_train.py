@@ -48,6 +48,14 @@ class GPUOps:
         return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
 
     @staticmethod
+    def relu_backward(gY, Y, bias_grad=True):
+        if gY.shape[1] <= 1024:
+            return gs.relu_backward(gY if gY.stride(-1) == 1 else gY.contiguous(), Y,
+                                    bias_grad=bias_grad)
+        g = gY * (Y > 0).to(gY.dtype)
+        return g, (g.sum(dim=0) if bias_grad else None)
+
+    @staticmethod
     def scatter_rows(n_rows: int, rows: gs.RowSelection, g: torch.Tensor) -> torch.Tensor:
         from .layers import _index_csr_cached
         full = torch.zeros((n_rows, g.shape[1]), dtype=torch.float32, device=g.device)
@@ -74,8 +82,11 @@ class _PartitionedPropagate(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gY):
         (Y,) = ctx.saved_tensors
-        g = gY if Y is None else gY * (Y > 0).to(gY.dtype)
-        g_bias = g.sum(dim=0) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        want_bias = ctx.has_bias and ctx.needs_input_grad[1]
+        if Y is None:
+            g, g_bias = gY, (gY.sum(dim=0) if want_bias else None)
+        else:
+            g, g_bias = ctx.ops.relu_backward(gY, Y, bias_grad=want_bias)
         g_Z = None
         if ctx.needs_input_grad[0]:
             part = ctx.part

@@ -100,8 +100,14 @@ class _CSRMatMul(torch.autograd.Function):
     def backward(ctx, gY):
         A, rows = ctx.A, ctx.rows
         (Y,) = ctx.saved_tensors
-        g = gY if Y is None else gY * (Y > 0).to(gY.dtype)
-        g_bias = g.sum(dim=0) if ctx.has_bias and ctx.needs_input_grad[1] else None
+        want_bias = ctx.has_bias and ctx.needs_input_grad[1]
+        if Y is not None and gY.shape[1] <= 1024:
+            # rectify mask and bias gradient in one pass (gcg_relu_backward_f32)
+            g, g_bias = gs.relu_backward(gY.contiguous() if gY.stride(-1) != 1 else gY, Y,
+                                         bias_grad=want_bias)
+        else:
+            g = gY if Y is None else gY * (Y > 0).to(gY.dtype)
+            g_bias = g.sum(dim=0) if want_bias else None
         g_Z = None
         if ctx.needs_input_grad[0]:
             if rows is not None:
@@ -110,7 +116,7 @@ class _CSRMatMul(torch.autograd.Function):
                 # within fp32 rounding
                 g_Z = gs.spmm(A.rows_transpose(rows), g.contiguous(), mode=ctx.mode)
             else:
-                g_Z = gs.spmm(A.transpose(), g.contiguous(), mode=ctx.mode)
+                g_Z = A.tmatmul(g.contiguous(), mode=ctx.mode)
         return g_Z, g_bias, None, None, None, None
 
 

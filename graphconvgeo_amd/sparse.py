@@ -31,6 +31,13 @@ MODES = ("auto", "fast", "ordered", "rowwise")
 # whole launch (then rows are split, 'fast'): longest-first scheduling hides a row of up
 # to ~nnz/2048 nonzeros behind the bulk (Twitter-World: 12,189 of 41.4M, measured equal).
 AUTO_SPLIT_RATIO = 2048
+# DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
+# the dense MFMA GEMM -- break-even is ~5-10 % (a gathered nonzero ~200 ps, a dense element
+# ~10-20 ps at Twitter-World, tools/exp_xtg_head.py); at most HYBRID_MAX_COLS of them, and only
+# for matrices of at least HYBRID_MIN_ROWS rows (below that everything is cache-resident).
+HYBRID_MIN_DENSITY = 0.05
+HYBRID_MAX_COLS = 256
+HYBRID_MIN_ROWS = 65536
 
 
 def _stream_handle(device: torch.device) -> C.c_void_p:
@@ -253,6 +260,72 @@ class DeviceCSR:
             cache[rows.key] = t
         return t
 
+    def _dense_column_split(self):
+        """The columns dense enough that A^T . G is cheaper as a dense MFMA product.
+
+        A bag-of-words X (data.py:378-397) has Zipf column frequencies: a few hundred words
+        carry about half the nonzeros. In X^T . G (the W1 gradient, grad of mlpconv.py:71)
+        every nonzero gathers one K-wide row of G from HBM (~200 ps per nonzero at
+        Twitter-World), while X_head^T . G on the split-K MFMA GEMM streams G once and costs
+        ~10-20 ps per (row, column) element -- so columns with density >= HYBRID_MIN_DENSITY
+        (at most HYBRID_MAX_COLS of them, the most frequent) move to a dense N x Fh block and
+        the rest stay a CSR gather. Built once per matrix on the device; None if no column
+        qualifies (H: its densest column is a hub at <= 1 % of N)."""
+        if "_dense_split" in self.__dict__:
+            return self._dense_split
+        split = None
+        n, F = self.shape
+        thr = max(1, int(np.ceil(HYBRID_MIN_DENSITY * n)))
+        if self.nnz and n >= HYBRID_MIN_ROWS:
+            cols64 = self.indices.to(torch.int64)
+            counts = torch.bincount(cols64, minlength=F)
+            cand = torch.nonzero(counts >= thr).flatten()
+            if cand.numel() > HYBRID_MAX_COLS:
+                cand = cand[torch.topk(counts[cand], HYBRID_MAX_COLS).indices]
+            if cand.numel():
+                cand = torch.sort(cand).values
+                fh = int(cand.numel())
+                slot = torch.full((F,), -1, dtype=torch.int64, device=self.device)
+                slot[cand] = torch.arange(fh, device=self.device)
+                s = slot[cols64]
+                del cols64
+                head = s >= 0
+                lens = (self.indptr[1:] - self.indptr[:-1]).to(torch.int64)
+                row = torch.repeat_interleave(torch.arange(n, device=self.device), lens,
+                                              output_size=self.nnz)
+                Xh = empty_dense(n, fh, self.device)
+                Xh.zero_()
+                Xh[row[head], s[head]] = self.data[head]
+                del row, s
+                keep = ~head
+                c = torch.zeros(self.nnz + 1, dtype=torch.int64, device=self.device)
+                torch.cumsum(keep, 0, out=c[1:])
+                tail = DeviceCSR(c[self.indptr.to(torch.int64)].to(torch.int32),
+                                 self.indices[keep], self.data[keep], self.shape, validate=False)
+                split = (cand, Xh, tail.transpose())
+                tail._transpose = None
+        self._dense_split = split
+        return split
+
+    def tmatmul(self, G: torch.Tensor, mode: str = "auto",
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """A^T . G (the gradient of S.dot(A, Z) w.r.t. Z). 'rowwise' / 'ordered' (and 'auto'
+        wherever the transpose would run bitwise) gather through CSR(A^T); otherwise the
+        dense columns of A go through the MFMA GEMM (_dense_column_split): within fp32
+        rounding of the gather (a different summation order), not bitwise."""
+        T = self.transpose()
+        use_split = mode == "fast" or (
+            mode == "auto" and T.max_row_nnz() * AUTO_SPLIT_RATIO > max(T.nnz, 1))
+        split = self._dense_column_split() if use_split else None
+        if split is None:
+            return spmm(T, G, mode=mode, out=out)
+        from . import dense
+        cols, Xh, tail_t = split
+        G = _check_dense(G, tail_t)
+        out = spmm(tail_t, G, mode=mode, out=out)
+        out.index_copy_(0, cols, dense.gemm_tn(Xh, G))
+        return out
+
     def __repr__(self):
         return f"DeviceCSR(shape={self.shape}, nnz={self.nnz}, device={self.device})"
 
@@ -353,6 +426,51 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
                  _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(ws),
                  0 if ws is None else ws.numel() * 4, stream)
     return out
+
+
+_RELU_WS: dict = {}
+
+
+def relu_backward(gY: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor] = None,
+                  bias_grad: bool = True):
+    """(g, db): g = gY where Y > 0 else 0 and db = column sums of g, one pass
+    (gcg_relu_backward_f32; the grad of rectify(. + b), mlpconv.py:75-77). out may be gY."""
+    _require_cuda(gY, "gY")
+    _require_cuda(Y, "Y")
+    M, K = gY.shape
+    if Y.shape != (M, K):
+        raise ValueError("gY and Y must have the same shape")
+    if out is None:
+        out = empty_dense(M, K, gY.device)
+    db = torch.empty(K, dtype=torch.float32, device=gY.device) if bias_grad else None
+    nb = C.c_size_t()
+    call("gcg_relu_backward_f32_workspace_bytes", M, K, C.byref(nb))
+    key = (gY.device, torch.cuda.current_stream(gY.device).cuda_stream)
+    ws = _RELU_WS.get(key)
+    if ws is None or ws.numel() * 4 < nb.value:
+        ws = torch.empty(max((nb.value + 3) // 4, 1), dtype=torch.float32, device=gY.device)
+        _RELU_WS[key] = ws
+
+    def ld(t):
+        return t.stride(0) if t.shape[0] > 1 else K
+
+    def rows16(t):
+        return (t.shape[0] <= 1 or t.stride(0) % 4 == 0) and t.data_ptr() % 16 == 0
+
+    if K > 256:  # the wide path loads dwordx4: stage unpadded operands into padded buffers
+        if not rows16(gY) or (K > 1 and gY.stride(1) != 1):
+            gY = empty_dense(M, K, gY.device).copy_(gY)
+        if not rows16(Y) or (K > 1 and Y.stride(1) != 1):
+            Y = empty_dense(M, K, Y.device).copy_(Y)
+        if not rows16(out):
+            raise ValueError("relu_backward: out needs 16-B aligned rows when K > 256")
+    for t in (gY, Y, out):
+        if K > 1 and t.stride(1) != 1:
+            raise ValueError("relu_backward operands need unit column stride")
+    with torch.cuda.device(gY.device):
+        call("gcg_relu_backward_f32", M, K, _ptr(gY), ld(gY), _ptr(Y), ld(Y), _ptr(out), ld(out),
+             _ptr(db), _ptr(ws), ws.numel() * 4, _stream_handle(gY.device))
+    return out, db
 
 
 def index_csr(idx: torch.Tensor, n_rows: int):

@@ -148,6 +148,18 @@ gcg_status gcg_scatter_add_rows_f32(int64_t n_rows, const int32_t* seg_ptr,
                                     int64_t K, float* out, int64_t ldo, gcg_stream_t stream);
 
 /*
+ * Rectify backward with the bias gradient in one pass (Theano's grad of
+ * rectify(S.dot(H, Z) + b), mlpconv.py:75-77): g = gY where Y > 0 else 0 (g_out may alias gY),
+ * bias_grad[c] = sum_r g[r][c] (nullable; deterministic: per-block partials in the workspace,
+ * summed in block order). K <= 1024. The workspace (size from _workspace_bytes) is required.
+ */
+gcg_status gcg_relu_backward_f32_workspace_bytes(int64_t M, int64_t K, size_t* bytes);
+gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
+                                 const float* Y, int64_t ldy, float* g_out, int64_t ldo,
+                                 float* bias_grad /*nullable*/, void* workspace,
+                                 size_t workspace_bytes, gcg_stream_t stream);
+
+/*
  * CSR transpose on the device (CSR(X^T) for the X^T . dZ1 gradient of
  * mlpconv.py:71). Output is sorted by (row, col) with stable order for equal
  * entries. out_indptr int32[n_cols+1], out_indices int32[nnz], out_vals f32[nnz].

@@ -207,3 +207,24 @@ def test_gemm_tn_abi_without_gpu(native_lib):
     assert tn(8, 3, 5, a16, 3, b16, 8, None, c16, 5, None, 0, None) == 1      # lda < round4(M)
     assert tn(8, 3, 5, C.c_void_p(0x10008), 4, b16, 8, None, c16, 5, None, 0, None) == 2
     assert tn(8, 3, 5, a16, 4, b16, 8, None, c16, 4, None, 0, None) == 1      # ldc < N
+
+
+def test_relu_backward_abi_without_gpu(native_lib):
+    """Fused rectify backward + bias gradient: workspace sizing and host-side checks."""
+    import ctypes as C
+    lib = native_lib
+    nb = C.c_size_t()
+    assert lib.gcg_relu_backward_f32_workspace_bytes(840_000, 300, C.byref(nb)) == 0
+    assert nb.value == 4 * 300 * ((840_000 + 511) // 512)
+    assert lib.gcg_relu_backward_f32_workspace_bytes(-1, 3, C.byref(nb)) == 1
+    a16, b16, c16, w16 = (C.c_void_p(x) for x in (0x10000, 0x20000, 0x30000, 0x40000))
+    rb = lib.gcg_relu_backward_f32
+    assert rb(8, 1025, a16, 1028, b16, 1028, c16, 1028, None, w16, 1 << 20, None) == 1  # K cap
+    assert rb(8, 4, None, 4, b16, 4, c16, 4, None, w16, 1 << 20, None) == 1            # null gY
+    assert rb(8, 4, a16, 3, b16, 4, c16, 4, None, w16, 1 << 20, None) == 1             # ld < K
+    assert rb(8, 4, C.c_void_p(0x10002), 4, b16, 4, c16, 4, None, w16, 1 << 20, None) == 2
+    assert rb(8, 4, a16, 4, b16, 4, c16, 4, None, None, 0, None) == 6                  # workspace
+    assert rb(8, 4, a16, 4, b16, 4, c16, 4, None, w16, 4, None) == 6                   # too small
+    # K > 256 needs the dwordx4 path (16-B rows)
+    assert rb(8, 300, a16, 301, b16, 304, c16, 304, None, w16, 1 << 20, None) == 2
+    assert rb(0, 4, None, 4, None, 4, None, 4, None, None, 0, None) == 0               # empty

@@ -130,6 +130,11 @@ class _CPUOps:
         return torch.from_numpy(O.spmm_f32(A, Z.numpy(), bias=b, act=act, rows=r))
 
     @staticmethod
+    def relu_backward(gY, Y, bias_grad=True):
+        g = gY * (Y > 0).to(gY.dtype)
+        return g, (g.sum(dim=0) if bias_grad else None)
+
+    @staticmethod
     def scatter_rows(n_rows, rows, g):
         from oracle import gcn_oracle as O
         out = np.zeros((n_rows, g.shape[1]), np.float32)
