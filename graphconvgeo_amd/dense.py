@@ -154,6 +154,67 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
     return out
 
 
+# -- weight gradients on a side stream -------------------------------------------------------
+# A weight gradient (A^T . G, MFMA-bound) has no consumer until the optimizer, while the rest
+# of the backward is a chain of HBM-bound CSR gathers: the two overlap on the GPU when the
+# weight gradient runs on its own stream. The autograd engine runs each backward on the
+# stream its forward ran on, so W enters the consumer through an identity node created on the
+# side stream; the consumer's backward leaves (A, G, scale) in a slot and hands the identity
+# node a placeholder; the identity node's backward computes the gradient on the side stream.
+# The engine joins the streams (event waits) where gradients cross and at the end of
+# backward() -- also inside a HIP graph capture. The slot keeps A and G alive until the
+# autograd graph is freed, after that join.
+_SIDE_STREAMS: dict = {}
+SIDE_STREAM_WEIGHT_GRADS = True
+
+
+def _side_stream(device) -> torch.cuda.Stream:
+    s = _SIDE_STREAMS.get(device)
+    if s is None:
+        s = torch.cuda.Stream(device=device)
+        _SIDE_STREAMS[device] = s
+    return s
+
+
+class _Slot:
+    __slots__ = ("args",)
+
+    def __init__(self):
+        self.args = None
+
+
+class _SideWeightGrad(torch.autograd.Function):
+    """Identity on W; its backward computes scale * A^T . G (gemm_tn) from the slot."""
+
+    @staticmethod
+    def forward(ctx, W, slot):
+        ctx.slot = slot
+        return W.view_as(W)
+
+    @staticmethod
+    def backward(ctx, _placeholder):
+        if ctx.slot.args is None:  # the consumer produced no weight gradient
+            return None, None
+        A, G, scale = ctx.slot.args
+        return gemm_tn(A, G, scale=scale), None
+
+
+def _weight_on_side_stream(W: torch.Tensor):
+    """(W', slot): W' aliases W; the gradient reaching W' is computed on a side stream."""
+    if not (SIDE_STREAM_WEIGHT_GRADS and torch.is_grad_enabled() and W.requires_grad
+            and W.is_cuda):
+        return W, None
+    slot = _Slot()
+    with torch.cuda.stream(_side_stream(W.device)):
+        Wa = _SideWeightGrad.apply(W, slot)
+    return Wa, slot
+
+
+def _placeholder_grad(W: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
+    """A W-shaped gradient that costs no kernel (the real one is computed from the slot)."""
+    return like.new_empty(()).expand(W.shape)
+
+
 class _MatMul(torch.autograd.Function):
     """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88) and its gradients. Forward and dA = g . W^T
     are plain GEMMs (hipBLASLt, measured faster on these shapes); the weight gradient
@@ -161,28 +222,35 @@ class _MatMul(torch.autograd.Function):
     (gemm_tn, 1.13-1.28x hipBLASLt at Twitter-World shapes)."""
 
     @staticmethod
-    def forward(ctx, A, W, b):
+    def forward(ctx, A, W, b, slot=None):
         C = torch.matmul(A, W) if b is None else torch.addmm(b, A, W)
         ctx.save_for_backward(A, W)
         ctx.has_b = b is not None
+        ctx.slot = slot
         return C
 
     @staticmethod
     def backward(ctx, g):
         A, W = ctx.saved_tensors
         gA = gW = gb = None
-        if ctx.needs_input_grad[0]:
-            gA = torch.matmul(g, W.t())
-        if ctx.needs_input_grad[1]:
-            gW = gemm_tn(A, g)
         if ctx.has_b and ctx.needs_input_grad[2]:
             gb = g.sum(dim=0)
-        return gA, gW, gb
+        if ctx.needs_input_grad[1]:
+            if ctx.slot is not None:  # computed on the side stream (_SideWeightGrad)
+                ctx.slot.args = (A, g, None)
+                gW = _placeholder_grad(W, g)
+            else:
+                gW = gemm_tn(A, g)
+        if ctx.needs_input_grad[0]:
+            gA = torch.matmul(g, W.t())
+        return gA, gW, gb, None
 
 
 def matmul(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Differentiable A . W (+ b) with the weight gradient on the split-K MFMA kernel."""
-    return _MatMul.apply(A, W, b)
+    """Differentiable A . W (+ b); the weight gradient runs on the split-K MFMA kernel, on a
+    side stream so it overlaps the rest of the backward."""
+    Wa, slot = _weight_on_side_stream(W)
+    return _MatMul.apply(A, Wa, b, slot)
 
 
 class Projection:
@@ -206,7 +274,8 @@ class Projection:
             correct = torch.empty(M, dtype=torch.float32, device=P.device)
             _fused(P, self.fwd.get(W, False), b, y, 1.0, None, None, loss_rows, correct)
             return loss_rows.sum() / D, correct.sum() / D
-        return _ProjectXent.apply(P, W, b, labels, self, denom)
+        Wa, slot = _weight_on_side_stream(W)
+        return _ProjectXent.apply(P, Wa, b, labels, self, denom, slot)
 
     def probabilities(self, P, W, b) -> torch.Tensor:
         """softmax(P . W + b) rows (predict_proba) in one fused launch."""
@@ -252,7 +321,7 @@ class _ProjectXent(torch.autograd.Function):
     dP = G . (g W)^T (hipBLASLt), dW = g P^T . G (split-K MFMA gemm_tn), db = g colsum(G)."""
 
     @staticmethod
-    def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None):
+    def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None, slot=None):
         P = _aligned_operand(P, "P")
         M, N = P.shape[0], W.shape[1]
         D = float(max(M if denom is None else denom, 1))  # rows the mean is over (all ranks)
@@ -264,6 +333,7 @@ class _ProjectXent(torch.autograd.Function):
         _fused(P, proj.fwd.get(W, False), b, y, 1.0 / D, None, G, loss_rows, correct)
         ctx.save_for_backward(P, W, G)
         ctx.proj = proj
+        ctx.slot = slot
         ctx.has_b = b is not None
         loss = loss_rows.sum() / D
         acc = correct.sum() / D
@@ -275,14 +345,20 @@ class _ProjectXent(torch.autograd.Function):
         P, W, G = ctx.saved_tensors
         gP = gW = gb = None
         g = g_loss.reshape(())
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = G.sum(dim=0).mul_(g)
+        if ctx.needs_input_grad[1]:
+            # split-K MFMA, the upstream gradient applied on device; on the side stream when
+            # W came through _weight_on_side_stream
+            if ctx.slot is not None:
+                ctx.slot.args = (P, G, g)
+                gW = _placeholder_grad(W, g)
+            else:
+                gW = gemm_tn(P, G, scale=g)
         if ctx.needs_input_grad[0]:
             # plain GEMM: hipBLASLt measured faster here (4.3 vs 5.2 ms at 840k x 930 x 300)
             gP = torch.matmul(G, (W.detach() * g).t())
-        if ctx.needs_input_grad[1]:
-            gW = gemm_tn(P, G, scale=g)  # split-K MFMA, the upstream gradient applied on device
-        if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = G.sum(dim=0).mul_(g)
-        return gP, gW, gb, None, None, None
+        return gP, gW, gb, None, None, None, None
 
 
 def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct):
@@ -335,7 +411,8 @@ def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None,
     """(mean CE loss, accuracy) of softmax(P . W + b) against labels, differentiable in P, W, b.
     denom: the row count the mean is taken over (default: these rows; the total over all
     ranks when each rank holds a share of the targets)."""
-    return _ProjectXent.apply(P, W, b, labels, proj or Projection(), denom)
+    Wa, slot = _weight_on_side_stream(W)
+    return _ProjectXent.apply(P, Wa, b, labels, proj or Projection(), denom, slot)
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int] = None

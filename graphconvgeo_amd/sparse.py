@@ -322,8 +322,15 @@ class DeviceCSR:
         from . import dense
         cols, Xh, tail_t = split
         G = _check_dense(G, tail_t)
+        # the MFMA head product on a side stream, overlapping the HBM-bound tail gather
+        main = torch.cuda.current_stream(self.device)
+        side = dense._side_stream(self.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            head = dense.gemm_tn(Xh, G)
         out = spmm(tail_t, G, mode=mode, out=out)
-        out.index_copy_(0, cols, dense.gemm_tn(Xh, G))
+        main.wait_stream(side)
+        out.index_copy_(0, cols, head)
         return out
 
     def __repr__(self):

@@ -193,3 +193,35 @@ def test_gemm_tn_strided_views(cuda):
     Bbuf.copy_(torch.from_numpy(B))
     C = dense.gemm_tn(torch.from_numpy(A).to(cuda), Bbuf).cpu().numpy()
     _check_gemm(C, A.T.copy(), B)
+
+
+def _weight_grads(cuda, side: bool, shared_w: bool):
+    """W used by project_softmax_xent and (optionally) a second matmul; gradients accumulate."""
+    old = dense.SIDE_STREAM_WEIGHT_GRADS
+    dense.SIDE_STREAM_WEIGHT_GRADS = side
+    try:
+        M, K, N = 3000, 300, 129
+        P, W, b = _rand((M, K), 41, 0.2), _rand((K, N), 42, 0.2), _rand((N,), 43, 0.1)
+        y = torch.from_numpy(np.random.default_rng(44).integers(0, N, M)).to(cuda)
+        Pt = torch.from_numpy(P).to(cuda).requires_grad_()
+        Wt = torch.from_numpy(W).to(cuda).requires_grad_()
+        bt = torch.from_numpy(b).to(cuda).requires_grad_()
+        Wt.grad = torch.full_like(Wt, 0.25)  # accumulate into an existing gradient
+        loss, _ = dense.project_softmax_xent(Pt, Wt, bt, y)
+        if shared_w:
+            loss = loss + dense.matmul(Pt * 1.5, Wt).square().mean()
+        (loss * 3.0).backward()
+        torch.cuda.synchronize()
+        return Pt.grad.clone(), Wt.grad.clone(), bt.grad.clone()
+    finally:
+        dense.SIDE_STREAM_WEIGHT_GRADS = old
+
+
+@pytest.mark.parametrize("shared_w", [False, True])
+def test_side_stream_weight_grads_equal_inline(cuda, shared_w):
+    """The weight gradient computed on the side stream (overlapping the rest of the backward)
+    is bitwise the inline one, also when W feeds two products and W.grad already exists."""
+    a = _weight_grads(cuda, True, shared_w)
+    b = _weight_grads(cuda, False, shared_w)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
