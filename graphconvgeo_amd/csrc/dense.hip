@@ -487,6 +487,7 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
   const int j = lane & 15, q = lane >> 4;
   const int m0 = blockIdx.x * (64 * MG);
   const int n0 = blockIdx.y * (256 * NG) + wave * (64 * NG);
+  if (n0 >= N) return;  // a wave wholly past N (no LDS, no barriers: safe to leave early)
   const int t_begin = blockIdx.z * rows_per_split;
   const int t_end = min(R, t_begin + rows_per_split);
   const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
@@ -599,7 +600,10 @@ struct TnPlan {
 
 TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   TnPlan p;
-  p.mg = 1, p.ng = 2, p.pd = 8;
+  // NG = 2 (4 + 4 dwordx4 loads feed 32 MFMAs) unless N is narrow: a workgroup spans 256*NG
+  // columns and its waves past N leave at once, so N <= 512 runs more busy waves with NG = 1
+  // (1.4M x 300 x 256: 2.49 vs 4.38 ms; x 930: NG = 2 87.7 vs 82.5 TFLOP/s)
+  p.mg = 1, p.ng = N > 512 ? 2 : 1, p.pd = 8;
   if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD"
     int a = 0, b = 0, c = 0;
     if (std::sscanf(v, "%d,%d,%d", &a, &b, &c) == 3) p.mg = a, p.ng = b, p.pd = c;

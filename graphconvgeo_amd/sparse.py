@@ -32,10 +32,11 @@ MODES = ("auto", "fast", "ordered", "rowwise")
 # to ~nnz/2048 nonzeros behind the bulk (Twitter-World: 12,189 of 41.4M, measured equal).
 AUTO_SPLIT_RATIO = 2048
 # DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
-# the dense MFMA GEMM -- break-even is ~5-10 % (a gathered nonzero ~200 ps, a dense element
-# ~10-20 ps at Twitter-World, tools/exp_xtg_head.py); at most HYBRID_MAX_COLS of them, and only
+# the dense MFMA GEMM -- break-even is ~1.5-2 % (a gathered nonzero ~190 ps, a dense element
+# ~3-9 ps at Twitter-World, tools/exp_xtg_head.py / exp_tn_shapes.py); at most HYBRID_MAX_COLS
+# of them (the GEMM's cost grows faster than the gather it saves beyond), and only
 # for matrices of at least HYBRID_MIN_ROWS rows (below that everything is cache-resident).
-HYBRID_MIN_DENSITY = 0.05
+HYBRID_MIN_DENSITY = 0.02
 HYBRID_MAX_COLS = 256
 HYBRID_MIN_ROWS = 65536
 
@@ -279,12 +280,13 @@ class DeviceCSR:
         if self.nnz and n >= HYBRID_MIN_ROWS:
             cols64 = self.indices.to(torch.int64)
             counts = torch.bincount(cols64, minlength=F)
-            cand = torch.nonzero(counts >= thr).flatten()
-            if cand.numel() > HYBRID_MAX_COLS:
-                cand = cand[torch.topk(counts[cand], HYBRID_MAX_COLS).indices]
-            if cand.numel():
+            q = int((counts >= thr).sum())
+            if q:
+                # the GEMM computes columns in groups of 64 anyway: fill the last group with
+                # the next most frequent columns (free in the GEMM, fewer gathered nonzeros)
+                fh = min((q + 63) // 64 * 64, HYBRID_MAX_COLS, F)
+                cand = torch.topk(counts, fh, sorted=False).indices
                 cand = torch.sort(cand).values
-                fh = int(cand.numel())
                 slot = torch.full((F,), -1, dtype=torch.int64, device=self.device)
                 slot[cand] = torch.arange(fh, device=self.device)
                 s = slot[cols64]
@@ -322,15 +324,17 @@ class DeviceCSR:
         from . import dense
         cols, Xh, tail_t = split
         G = _check_dense(G, tail_t)
-        # the MFMA head product on a side stream, overlapping the HBM-bound tail gather
+        # the MFMA head product on a side stream, overlapping the HBM-bound tail gather;
+        # computed as (G^T . X_head)^T: K (300) x Fh (a multiple of 64) tiles the split-K
+        # kernel with no idle waves (2.5 ms vs 3.7 ms for X_head^T . G at Twitter-World)
         main = torch.cuda.current_stream(self.device)
         side = dense._side_stream(self.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            head = dense.gemm_tn(Xh, G)
+            head_t = dense.gemm_tn(G, Xh)
         out = spmm(tail_t, G, mode=mode, out=out)
         main.wait_stream(side)
-        out.index_copy_(0, cols, head)
+        out.index_copy_(0, cols, head_t.t())
         return out
 
     def __repr__(self):
