@@ -45,6 +45,7 @@ SIGNATURES = {
     "gcg_index_csr": (C.c_int, [_i64, _p, _i64, _p, _p, _p, C.c_size_t, _psz, _p]),
     "gcg_scatter_add_rows_f32": (C.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p]),
     "gcg_relu_backward_f32_workspace_bytes": (C.c_int, [_i64, _i64, _psz]),
+    "gcg_column_sum_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, _p, C.c_size_t, _p]),
     "gcg_relu_backward_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p,
                                         C.c_size_t, _p]),
     "gcg_csr_transpose_f32": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _p, _p, _p,

@@ -95,28 +95,37 @@ gcg_status sort_pairs_ws(int64_t n, int end_bit, size_t* temp_bytes) {
 // Rectify backward + bias gradient in one pass (Theano's grad of
 // rectify(S.dot(H, Z) + b), mlpconv.py:75-77): g = gY where Y > 0 else 0, written to g_out
 // (may alias gY), and per-block column partial sums of g. Block = 4 waves; wave w takes rows
-// r0 + w, r0 + w + 4, ...; lanes span the columns in dwordx4 (or dword) pieces.
-constexpr int kReluRows = 512;  // rows per block
-constexpr int kReluMaxK4 = 4;   // dwordx4 column pieces per lane (K <= 1024 on the vector path)
+// r0 + w, r0 + w + 4, ...; lanes span the columns in dwordx4 (or dword) pieces. MASK = false:
+// column sums of gY only (Y and g_out unused) -- the bias gradient of a dense projection.
+constexpr int kReluMinRows = 512;   // rows per block at least ...
+constexpr int kReluMaxBlocks = 1024;  // ... and at most this many blocks (partial rows)
+constexpr int kReluMaxK4 = 4;       // dwordx4 column pieces per lane (K <= 1024 on the vector path)
 
-template <int VEC>
+int64_t relu_rows_per_block(int64_t M) {
+  const int64_t r = (M + kReluMaxBlocks - 1) / kReluMaxBlocks;
+  return std::max<int64_t>(kReluMinRows, (r + 3) / 4 * 4);
+}
+
+template <int VEC, bool MASK>
 __global__ __launch_bounds__(256) void relu_backward_kernel(
-    int64_t M, int K, const float* gY, int64_t ldg, const float* __restrict__ Y, int64_t ldy,
-    float* g_out, int64_t ldo, float* __restrict__ partial) {
+    int64_t M, int K, int64_t rows_per_block, const float* gY, int64_t ldg,
+    const float* __restrict__ Y, int64_t ldy, float* g_out, int64_t ldo,
+    float* __restrict__ partial) {
   __shared__ float red[4][kReluMaxK4 * 64 * 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * kReluRows;
-  const int64_t r1 = min(M, r0 + kReluRows);
+  const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
+  const int64_t r1 = min(M, r0 + rows_per_block);
   const int pieces = (K + 64 * VEC - 1) / (64 * VEC);
   float acc[kReluMaxK4][VEC];
 #pragma unroll
   for (int p = 0; p < kReluMaxK4; ++p)
 #pragma unroll
     for (int e = 0; e < VEC; ++e) acc[p][e] = 0.f;
+#pragma unroll 2
   for (int64_t r = r0 + w; r < r1; r += 4) {
     const float* gr = gY + r * ldg;
-    const float* yr = Y + r * ldy;
-    float* orow = g_out + r * ldo;
+    const float* yr = MASK ? Y + r * ldy : nullptr;
+    float* orow = MASK ? g_out + r * ldo : nullptr;
 #pragma unroll
     for (int p = 0; p < kReluMaxK4; ++p) {
       if (p >= pieces) break;
@@ -126,21 +135,29 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
         if (c + 4 > K) {  // ragged tail: element-wise, never touches columns >= K
           for (int e = 0; e < 4; ++e)
             if (c + e < K) {
-              const float o = yr[c + e] > 0.f ? gr[c + e] : 0.f;
-              orow[c + e] = o;
+              float o = gr[c + e];
+              if constexpr (MASK) {
+                o = yr[c + e] > 0.f ? o : 0.f;
+                orow[c + e] = o;
+              }
               acc[p][e] += o;
             }
           continue;
         }
-        const float4 gv = *reinterpret_cast<const float4*>(gr + c);
-        const float4 yv = *reinterpret_cast<const float4*>(yr + c);
-        const float4 o = make_float4(yv.x > 0.f ? gv.x : 0.f, yv.y > 0.f ? gv.y : 0.f,
-                                     yv.z > 0.f ? gv.z : 0.f, yv.w > 0.f ? gv.w : 0.f);
-        *reinterpret_cast<float4*>(orow + c) = o;
+        float4 o = *reinterpret_cast<const float4*>(gr + c);
+        if constexpr (MASK) {
+          const float4 yv = *reinterpret_cast<const float4*>(yr + c);
+          o = make_float4(yv.x > 0.f ? o.x : 0.f, yv.y > 0.f ? o.y : 0.f,
+                          yv.z > 0.f ? o.z : 0.f, yv.w > 0.f ? o.w : 0.f);
+          *reinterpret_cast<float4*>(orow + c) = o;
+        }
         acc[p][0] += o.x; acc[p][1] += o.y; acc[p][2] += o.z; acc[p][3] += o.w;
       } else {
-        const float o = yr[c] > 0.f ? gr[c] : 0.f;
-        orow[c] = o;
+        float o = gr[c];
+        if constexpr (MASK) {
+          o = yr[c] > 0.f ? o : 0.f;
+          orow[c] = o;
+        }
         acc[p][0] += o;
       }
     }
@@ -157,15 +174,26 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
   }
 }
 
-// bias_grad[c] = sum over blocks (in order) of partial[b][c]
-__global__ __launch_bounds__(256) void column_sum_kernel(int64_t n_blocks, int K,
+// out[c] = sum over the partial rows of partial[b][c], in a fixed order: workgroup = 16 waves
+// over 64 columns; wave w sums rows w, w + 16, ... in order, then wave 0 adds the 16 in order.
+__global__ __launch_bounds__(1024) void column_sum_kernel(int64_t n_blocks, int K,
                                                          const float* __restrict__ partial,
                                                          float* __restrict__ out) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= K) return;
+  __shared__ float red[16][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + lane;
+  const int cc = c < K ? c : K - 1;
   float s = 0.f;
-  for (int64_t b = 0; b < n_blocks; ++b) s += partial[b * K + c];
-  out[c] = s;
+#pragma unroll 4
+  for (int64_t b = w; b < n_blocks; b += 16) s += partial[b * K + cc];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && c < K) {
+    float t = red[0][lane];
+#pragma unroll
+    for (int i = 1; i < 16; ++i) t += red[i][lane];
+    out[c] = t;
+  }
 }
 
 }  // namespace
@@ -281,53 +309,79 @@ gcg_status gcg_csr_transpose_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
 gcg_status gcg_relu_backward_f32_workspace_bytes(int64_t M, int64_t K, size_t* bytes) {
   if (M < 0 || K < 0 || bytes == nullptr)
     return fail(GCG_ERR_INVALID_ARG, "gcg_relu_backward_f32_workspace_bytes: bad args");
-  *bytes = sizeof(float) * static_cast<size_t>((M + kReluRows - 1) / kReluRows) * K;
+  const int64_t rpb = relu_rows_per_block(M);
+  *bytes = sizeof(float) * static_cast<size_t>((M + rpb - 1) / rpb) * K;
   return GCG_OK;
 }
 
-gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
-                                 const float* Y, int64_t ldy, float* g_out, int64_t ldo,
-                                 float* bias_grad, void* workspace, size_t workspace_bytes,
-                                 gcg_stream_t stream) {
-  const char* fn = "gcg_relu_backward_f32";
+namespace {
+
+// shared by gcg_relu_backward_f32 (MASK) and gcg_column_sum_f32 (no mask)
+gcg_status relu_colsum(const char* fn, bool mask, int64_t M, int64_t K, const float* gY,
+                       int64_t ldg, const float* Y, int64_t ldy, float* g_out, int64_t ldo,
+                       float* bias_grad, void* workspace, size_t workspace_bytes,
+                       gcg_stream_t stream) {
   if (M < 0 || K < 0 || K > 64 * 4 * kReluMaxK4)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld K=%lld (K <= %d)", fn,
                 static_cast<long long>(M), static_cast<long long>(K), 64 * 4 * kReluMaxK4);
+  auto st = static_cast<hipStream_t>(stream);
   if (M == 0 || K == 0) {
     if (bias_grad != nullptr && K > 0)
-      GCG_HIP_CHECK(hipMemsetAsync(bias_grad, 0, sizeof(float) * K, static_cast<hipStream_t>(stream)));
+      GCG_HIP_CHECK(hipMemsetAsync(bias_grad, 0, sizeof(float) * K, st));
     return GCG_OK;
   }
-  if (gY == nullptr || Y == nullptr || g_out == nullptr)
+  if (gY == nullptr || (mask && (Y == nullptr || g_out == nullptr)) ||
+      (!mask && bias_grad == nullptr))
     return fail(GCG_ERR_INVALID_ARG, "%s: null operand", fn);
-  if (ldg < K || ldy < K || ldo < K) return fail(GCG_ERR_INVALID_ARG, "%s: ld < K", fn);
-  if (!aligned(gY, 4) || !aligned(Y, 4) || !aligned(g_out, 4))
+  if (ldg < K || (mask && (ldy < K || ldo < K)))
+    return fail(GCG_ERR_INVALID_ARG, "%s: ld < K", fn);
+  if (!aligned(gY, 4) || (mask && (!aligned(Y, 4) || !aligned(g_out, 4))))
     return fail(GCG_ERR_MISALIGNED, "%s: operand not 4-B aligned", fn);
-  const int64_t n_blocks = (M + kReluRows - 1) / kReluRows;
+  const int64_t rpb = relu_rows_per_block(M);
+  const int64_t n_blocks = (M + rpb - 1) / rpb;
   const size_t need = sizeof(float) * static_cast<size_t>(n_blocks) * K;
   if (workspace == nullptr || workspace_bytes < need)  // the kernel always writes partials
     return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu < %zu bytes", fn, workspace_bytes, need);
   if (!aligned(workspace, 4)) return fail(GCG_ERR_MISALIGNED, "%s: workspace alignment", fn);
   float* part = static_cast<float*>(workspace);
-  auto st = static_cast<hipStream_t>(stream);
-  const bool vec = ldg % 4 == 0 && ldy % 4 == 0 && ldo % 4 == 0 &&
-                   aligned(gY, 16) && aligned(Y, 16) && aligned(g_out, 16);
+  const bool vec = ldg % 4 == 0 && aligned(gY, 16) &&
+                   (!mask || (ldy % 4 == 0 && ldo % 4 == 0 && aligned(Y, 16) && aligned(g_out, 16)));
   if (!vec && K > 64 * kReluMaxK4)
     return fail(GCG_ERR_MISALIGNED, "%s: K > %d needs 16-B rows (ld %% 4 == 0)", fn,
                 64 * kReluMaxK4);
-  if (vec)
-    hipLaunchKernelGGL(relu_backward_kernel<4>, dim3(static_cast<unsigned>(n_blocks)), dim3(256),
-                       0, st, M, int(K), gY, ldg, Y, ldy, g_out, ldo, part);
-  else
-    hipLaunchKernelGGL(relu_backward_kernel<1>, dim3(static_cast<unsigned>(n_blocks)), dim3(256),
-                       0, st, M, int(K), gY, ldg, Y, ldy, g_out, ldo, part);
+  const dim3 grid(static_cast<unsigned>(n_blocks));
+#define GCG_RELU_LAUNCH(V, MK)                                                                  \
+  hipLaunchKernelGGL((relu_backward_kernel<V, MK>), grid, dim3(256), 0, st, M, int(K), rpb, gY, \
+                     ldg, Y, ldy, g_out, ldo, part)
+  if (vec) {
+    if (mask) GCG_RELU_LAUNCH(4, true); else GCG_RELU_LAUNCH(4, false);
+  } else {
+    if (mask) GCG_RELU_LAUNCH(1, true); else GCG_RELU_LAUNCH(1, false);
+  }
+#undef GCG_RELU_LAUNCH
   GCG_HIP_CHECK(hipGetLastError());
   if (bias_grad != nullptr) {
-    hipLaunchKernelGGL(column_sum_kernel, dim3(static_cast<unsigned>((K + 255) / 256)), dim3(256),
+    hipLaunchKernelGGL(column_sum_kernel, dim3(static_cast<unsigned>((K + 63) / 64)), dim3(1024),
                        0, st, n_blocks, int(K), part, bias_grad);
     GCG_HIP_CHECK(hipGetLastError());
   }
   return GCG_OK;
+}
+
+}  // namespace
+
+gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
+                                 const float* Y, int64_t ldy, float* g_out, int64_t ldo,
+                                 float* bias_grad, void* workspace, size_t workspace_bytes,
+                                 gcg_stream_t stream) {
+  return relu_colsum("gcg_relu_backward_f32", true, M, K, gY, ldg, Y, ldy, g_out, ldo, bias_grad,
+                     workspace, workspace_bytes, stream);
+}
+
+gcg_status gcg_column_sum_f32(int64_t M, int64_t K, const float* X, int64_t ldx, float* out,
+                              void* workspace, size_t workspace_bytes, gcg_stream_t stream) {
+  return relu_colsum("gcg_column_sum_f32", false, M, K, X, ldx, nullptr, 0, nullptr, 0, out,
+                     workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

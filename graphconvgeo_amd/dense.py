@@ -28,7 +28,7 @@ import ctypes as C
 import torch
 
 from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call
-from .sparse import _ptr, _require_cuda, _stream_handle, empty_dense
+from .sparse import _ptr, _require_cuda, _stream_handle, column_sum, empty_dense
 
 FUSED_MAX_COLS = 1024
 ROWS_MAX_COLS = 4096
@@ -210,6 +210,11 @@ def _weight_on_side_stream(W: torch.Tensor):
     return Wa, slot
 
 
+def _colsum(X: torch.Tensor) -> torch.Tensor:
+    """Bias gradient: deterministic HIP column sum (K <= 1024), else torch's reduction."""
+    return column_sum(X) if X.dim() == 2 and X.shape[1] <= 1024 else X.sum(dim=0)
+
+
 def _placeholder_grad(W: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
     """A W-shaped gradient that costs no kernel (the real one is computed from the slot)."""
     return like.new_empty(()).expand(W.shape)
@@ -234,7 +239,7 @@ class _MatMul(torch.autograd.Function):
         A, W = ctx.saved_tensors
         gA = gW = gb = None
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = g.sum(dim=0)
+            gb = _colsum(g)
         if ctx.needs_input_grad[1]:
             if ctx.slot is not None:  # computed on the side stream (_SideWeightGrad)
                 ctx.slot.args = (A, g, None)
@@ -346,7 +351,7 @@ class _ProjectXent(torch.autograd.Function):
         gP = gW = gb = None
         g = g_loss.reshape(())
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = G.sum(dim=0).mul_(g)
+            gb = _colsum(G).mul_(g)
         if ctx.needs_input_grad[1]:
             # split-K MFMA, the upstream gradient applied on device; on the side stream when
             # W came through _weight_on_side_stream

@@ -105,8 +105,12 @@ class _CSRMatMul(torch.autograd.Function):
             # rectify mask and bias gradient in one pass (gcg_relu_backward_f32)
             g, g_bias = gs.relu_backward(gY.contiguous() if gY.stride(-1) != 1 else gY, Y,
                                          bias_grad=want_bias)
+        elif Y is None:
+            g = gY
+            g_bias = (gs.column_sum(gY) if gY.shape[1] <= 1024 else gY.sum(dim=0)) \
+                if want_bias else None
         else:
-            g = gY if Y is None else gY * (Y > 0).to(gY.dtype)
+            g = gY * (Y > 0).to(gY.dtype)
             g_bias = g.sum(dim=0) if want_bias else None
         g_Z = None
         if ctx.needs_input_grad[0]:

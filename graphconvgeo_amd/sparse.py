@@ -442,6 +442,35 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
 _RELU_WS: dict = {}
 
 
+def _colsum_workspace(M: int, K: int, device) -> torch.Tensor:
+    """Partial-sum workspace of gcg_relu_backward_f32 / gcg_column_sum_f32, per stream."""
+    nb = C.c_size_t()
+    call("gcg_relu_backward_f32_workspace_bytes", M, K, C.byref(nb))
+    key = (device, torch.cuda.current_stream(device).cuda_stream)
+    ws = _RELU_WS.get(key)
+    if ws is None or ws.numel() * 4 < nb.value:
+        ws = torch.empty(max((nb.value + 3) // 4, 1), dtype=torch.float32, device=device)
+        _RELU_WS[key] = ws
+    return ws
+
+
+def column_sum(X: torch.Tensor) -> torch.Tensor:
+    """X.sum(0) for an M x K float32 matrix (K <= 1024), deterministic (gcg_column_sum_f32):
+    the bias gradients (colsum of the logits / pre-activation gradient)."""
+    _require_cuda(X, "X")
+    M, K = X.shape
+    if K > 1 and X.stride(1) != 1:
+        X = X.contiguous()
+    if K > 256 and M > 1 and (X.stride(0) % 4 or X.data_ptr() % 16):
+        X = empty_dense(M, K, X.device).copy_(X)
+    out = torch.empty(K, dtype=torch.float32, device=X.device)
+    ws = _colsum_workspace(M, K, X.device)
+    with torch.cuda.device(X.device):
+        call("gcg_column_sum_f32", M, K, _ptr(X), X.stride(0) if M > 1 else K, _ptr(out), _ptr(ws),
+             ws.numel() * 4, _stream_handle(X.device))
+    return out
+
+
 def relu_backward(gY: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor] = None,
                   bias_grad: bool = True):
     """(g, db): g = gY where Y > 0 else 0 and db = column sums of g, one pass
@@ -454,13 +483,7 @@ def relu_backward(gY: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor]
     if out is None:
         out = empty_dense(M, K, gY.device)
     db = torch.empty(K, dtype=torch.float32, device=gY.device) if bias_grad else None
-    nb = C.c_size_t()
-    call("gcg_relu_backward_f32_workspace_bytes", M, K, C.byref(nb))
-    key = (gY.device, torch.cuda.current_stream(gY.device).cuda_stream)
-    ws = _RELU_WS.get(key)
-    if ws is None or ws.numel() * 4 < nb.value:
-        ws = torch.empty(max((nb.value + 3) // 4, 1), dtype=torch.float32, device=gY.device)
-        _RELU_WS[key] = ws
+    ws = _colsum_workspace(M, K, gY.device)
 
     def ld(t):
         return t.stride(0) if t.shape[0] > 1 else K

@@ -160,6 +160,14 @@ gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t 
                                  size_t workspace_bytes, gcg_stream_t stream);
 
 /*
+ * Column sums out[c] = sum_r X[r][c] (the bias gradient of a dense projection, colsum of the
+ * logits gradient; Theano's grad of T.dot(h, W) + b, mlpconv.py:88-93), deterministic, same
+ * kernels and workspace (gcg_relu_backward_f32_workspace_bytes) as gcg_relu_backward_f32.
+ */
+gcg_status gcg_column_sum_f32(int64_t M, int64_t K, const float* X, int64_t ldx, float* out,
+                              void* workspace, size_t workspace_bytes, gcg_stream_t stream);
+
+/*
  * CSR transpose on the device (CSR(X^T) for the X^T . dZ1 gradient of
  * mlpconv.py:71). Output is sorted by (row, col) with stable order for equal
  * entries. out_indptr int32[n_cols+1], out_indices int32[nnz], out_vals f32[nnz].

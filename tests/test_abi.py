@@ -215,7 +215,9 @@ def test_relu_backward_abi_without_gpu(native_lib):
     lib = native_lib
     nb = C.c_size_t()
     assert lib.gcg_relu_backward_f32_workspace_bytes(840_000, 300, C.byref(nb)) == 0
-    assert nb.value == 4 * 300 * ((840_000 + 511) // 512)
+    assert nb.value == 4 * 300 * 1020  # at most 1024 partial rows (here 824 rows each) ...
+    assert lib.gcg_relu_backward_f32_workspace_bytes(5000, 300, C.byref(nb)) == 0
+    assert nb.value == 4 * 300 * 10     # ... of at least 512 rows each
     assert lib.gcg_relu_backward_f32_workspace_bytes(-1, 3, C.byref(nb)) == 1
     a16, b16, c16, w16 = (C.c_void_p(x) for x in (0x10000, 0x20000, 0x30000, 0x40000))
     rb = lib.gcg_relu_backward_f32
@@ -228,3 +230,14 @@ def test_relu_backward_abi_without_gpu(native_lib):
     # K > 256 needs the dwordx4 path (16-B rows)
     assert rb(8, 300, a16, 301, b16, 304, c16, 304, None, w16, 1 << 20, None) == 2
     assert rb(0, 4, None, 4, None, 4, None, 4, None, None, 0, None) == 0               # empty
+
+
+def test_column_sum_abi_without_gpu(native_lib):
+    import ctypes as C
+    cs = native_lib.gcg_column_sum_f32
+    a16, o16, w16 = (C.c_void_p(x) for x in (0x10000, 0x20000, 0x40000))
+    assert cs(8, 4, a16, 4, None, w16, 1 << 20, None) == 1           # null out
+    assert cs(8, 4, a16, 3, o16, w16, 1 << 20, None) == 1            # ld < K
+    assert cs(8, 1025, a16, 1028, o16, w16, 1 << 22, None) == 1      # K cap
+    assert cs(8, 4, a16, 4, o16, None, 0, None) == 6                 # workspace
+    assert cs(8, 300, a16, 301, o16, w16, 1 << 20, None) == 2        # wide needs 16-B rows

@@ -12,7 +12,7 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.mark.parametrize("M,K,ld", [(1, 1, 1), (7, 3, 3), (513, 64, 64), (1000, 255, 256),
-                                    (5000, 300, 300), (4097, 1024, 1024), (2000, 301, 304), (700, 301, 301),
+                                    (5000, 300, 300), (4097, 1024, 1024), (700_001, 300, 300), (2000, 301, 304), (700, 301, 301),
                                     (1025, 20, 24)])
 def test_relu_backward_matches_numpy(M, K, ld):
     rng = np.random.default_rng(M * 31 + K)
@@ -44,3 +44,16 @@ def test_relu_backward_empty():
     gY = torch.empty(0, 16, device="cuda")
     g, db = gs.relu_backward(gY, gY.clone())
     assert g.shape == (0, 16) and torch.equal(db, torch.zeros(16, device="cuda"))
+
+
+@pytest.mark.parametrize("M,K,ld", [(1, 1, 1), (3, 5, 5), (777, 930, 932), (600_001, 300, 300),
+                                    (4000, 1024, 1024), (9000, 301, 301)])
+def test_column_sum_matches_float64(M, K, ld):
+    rng = np.random.default_rng(M + K)
+    X = rng.standard_normal((M, ld)).astype(np.float32)
+    Xd = torch.from_numpy(X).cuda()[:, :K]
+    s = gs.column_sum(Xd)
+    ref = X[:, :K].astype(np.float64).sum(0)
+    np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=0,
+                               atol=2e-6 * np.abs(X[:, :K]).sum(0).max() + 1e-7)
+    assert torch.equal(s, gs.column_sum(Xd))  # deterministic
