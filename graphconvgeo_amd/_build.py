@@ -16,7 +16,7 @@ CSRC = os.path.join(PKG_DIR, "csrc")
 # SpGEMM, MFMA dense projection + softmax/xent, error/version helpers. Compiled in parallel, linked into one shared library.
 SOURCES = [os.path.join(CSRC, f) for f in
            ("spmm.hip", "csr_ops.hip", "graph_build.hip", "spgemm.hip", "dense.hip", "errors.cpp")]
-INTERNAL_HEADERS = [os.path.join(CSRC, h) for h in ("common.h", "index_kernels.h")]
+INTERNAL_HEADERS = [os.path.join(CSRC, h) for h in ("common.h", "index_kernels.h", "gemm_epilogue.inc")]
 HEADER = os.path.join(REPO_DIR, "include", "gcg_spmm.h")
 LIB = os.path.join(PKG_DIR, "libgcg_spmm.so")
 ARCH = os.environ.get("GCG_OFFLOAD_ARCH", "gfx950")

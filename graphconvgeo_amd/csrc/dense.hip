@@ -11,6 +11,8 @@
 //       (exact f32 in / f32 accumulate). EPI = 1 fuses the whole output row: bias, softmax,
 //       cross-entropy against int32 labels, first-index argmax, and writes either
 //       (softmax - onehot) * scale (the logits gradient) or the probabilities.
+//   gemm_bl_kernel<G, WC, EPI>       the same product with B staged through LDS and shared by
+//       4 row bands (the plain products' default; see pick_shape).
 //   softmax_xent_rows_kernel<NV>     the same row epilogue for logits that already exist
 //       (the reference order, where the logits come out of the H SpMM, mlpconv.py:90-94).
 //
@@ -63,6 +65,7 @@ __device__ __forceinline__ int reduce16_min(int v) {
 }
 
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
+
 
 template <int RT, int G, int WR, int WC, int EPI, int PF>
 __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void gemm_kernel(
@@ -226,174 +229,153 @@ __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void ge
     }
   }
 
-  // ---- epilogue ----
-  // lane holds, for row  row0 + wr*16*RT + 16t + 4q + r  and column  colw + 64g + 4j + e,
-  // the value acc[t][g][e][r].
-  f4 bv[G];
-#pragma unroll
-  for (int g = 0; g < G; ++g) {
-    bv[g] = f4{0.f, 0.f, 0.f, 0.f};
-    const int c = colw + 64 * g + 4 * j;
-    if (bias != nullptr) {
-      if (c < N) bv[g].x = bias[c];
-      if (c + 1 < N) bv[g].y = bias[c + 1];
-      if (c + 2 < N) bv[g].z = bias[c + 2];
-      if (c + 3 < N) bv[g].w = bias[c + 3];
-    }
-  }
+#include "gemm_epilogue.inc"
+}
 
-  if constexpr (EPI == 0) {
+// ---------------------------------------------------------------------------------------
+// gemm_bl_kernel<G, WC, EPI>: the same product and epilogues with B staged through LDS.
+// Workgroup = 4 row bands (WR = 4) x WC column waves, wave tile 16 rows x 64*G columns
+// (RT = 1), workgroup tile 64 x 64*G*WC. Per 32-deep k chunk the workgroup copies A[64 x 32]
+// and B[32 x BN] to LDS once; the 4 row bands share every B fragment, so B leaves L2 once per
+// 64 rows (gemm_kernel: once per 16*RT rows per wave) and a fragment read costs LDS latency
+// instead of L2 latency. The next chunk's loads are issued into registers before the current
+// chunk's MFMAs and written to LDS after them (one LDS buffer, two barriers per chunk).
+// LDS B image: row k at k*BN floats; lanes (j, q) of one ds_read_b128 group read rows
+// k0+4q+e, columns 4j..4j+3: BN % 16 == 0 keeps every 16-lane group on 64 distinct banks.
+// ---------------------------------------------------------------------------------------
+template <int G, int WC, int EPI>
+__global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
+    int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+    int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
+    const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows) {
+  constexpr int RT = 1, WR = 4;
+  constexpr int NT = 64 * WR * WC;
+  constexpr int BM = 16 * RT * WR;  // 64
+  constexpr int BN = 64 * G * WC;
+  constexpr int KC = BN >= 512 ? 16 : 32;  // k depth of one chunk: wide B -> fewer staging VGPRs
+  constexpr int KP = KC + 4;
+  constexpr int AT = BM * KC / 4 < NT ? BM * KC / 4 : NT;  // threads staging A (whole waves)
+  constexpr int A4 = BM * KC / 4 / AT;
+  constexpr int B4 = KC * BN / 4 / NT;
+  static_assert(AT % 64 == 0 && A4 >= 1 && BM * KC / 4 % AT == 0, "A chunk must split evenly");
+  static_assert(B4 >= 1 && KC * BN / 4 % NT == 0, "B chunk must split evenly");
+  static_assert(BN % 16 == 0, "conflict-free B fragment reads");
+  // NB = 2 LDS buffers (one barrier per chunk) for the 8-wave tiles, which hold a CU alone
+  // anyway; the 4-wave tiles keep one buffer (two barriers) so 2-3 workgroups share a CU
+  constexpr int NB = (WC >= 2 && (2 * (BM * KP + KC * BN) + 3 * WC * BM) * 4 <= 160 * 1024) ? 2 : 1;
+  __shared__ float As[NB][BM][KP];
+  __shared__ float Bs[NB][KC][BN];
+  __shared__ float red[3][WC][BM];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int j = lane & 15, q = lane >> 4;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int colb = blockIdx.y * BN;          // workgroup's first column
+  const int colw = colb + wc * G * 64;       // this wave's first column
+  const int n4 = (N + 3) & ~3;
+
+  f4 acc[RT][G][4];
 #pragma unroll
-    for (int t = 0; t < RT; ++t)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + wr * 16 * RT + 16 * t + 4 * q + r;
-        if (row >= M) continue;
-        float* crow = Cout + row * ldc;
+    for (int e = 0; e < 4; ++e) acc[0][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  // Branch-free staging loads (clamped addresses, zeroed by selects): see gemm_kernel.
+  const int kmax4 = (K - 1) & ~3;
+  f4 areg[A4], breg[B4];
+  const bool a_stager = tid < AT;  // wave-uniform
+  auto load_chunk = [&](int kc0) {
 #pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int c = colw + 64 * g + 4 * j;
-          if (c >= N) continue;
-          f4 v = {acc[t][g][0][r] + bv[g].x, acc[t][g][1][r] + bv[g].y,
-                  acc[t][g][2][r] + bv[g].z, acc[t][g][3][r] + bv[g].w};
-          if (act == GCG_ACT_RELU) {  // Theano rectify 0.5*(x+|x|), mlpconv.py:77
-            v.x = 0.5f * (v.x + fabsf(v.x)); v.y = 0.5f * (v.y + fabsf(v.y));
-            v.z = 0.5f * (v.z + fabsf(v.z)); v.w = 0.5f * (v.w + fabsf(v.w));
-          }
-          if (c + 3 < N) {
-            *reinterpret_cast<f4*>(crow + c) = v;
-          } else {
-            crow[c] = v.x;
-            if (c + 1 < N) crow[c + 1] = v.y;
-            if (c + 2 < N) crow[c + 2] = v.z;
-          }
-        }
-      }
-  } else {
-    // Whole row in this workgroup (host guarantees BN >= N, gridDim.y == 1). One 16-row
-    // MFMA tile at a time (4 rows per lane live), partial row results combined over the
-    // WC waves of the row band through LDS.
-    if (scale_dev != nullptr) scale *= *scale_dev;
-    const int rb = wr * 16 * RT;  // first row of this wave's band inside the block
+    for (int i = 0; i < A4; ++i) {
+      const int idx = (a_stager ? tid : tid - AT) + AT * i;  // non-stagers: a harmless copy
+      const int r = idx / (KC / 4), k = kc0 + (idx % (KC / 4)) * 4;
+      const int64_t gr = row0 + r;
+      const int64_t rr = gr < M ? gr : M - 1;
+      const int kk = k < kmax4 ? k : kmax4;
+      f4 v = *reinterpret_cast<const f4*>(A + rr * lda + kk);
+      const bool rowok = gr < M;
+      v.x = (rowok && k < K) ? v.x : 0.f;
+      v.y = (rowok && k + 1 < K) ? v.y : 0.f;
+      v.z = (rowok && k + 2 < K) ? v.z : 0.f;
+      v.w = (rowok && k + 3 < K) ? v.w : 0.f;
+      areg[i] = v;
+    }
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
-      float mx[4], sm[4], xy[4];
-      int am[4], yl[4];
+    for (int i = 0; i < B4; ++i) {
+      const int idx = tid + NT * i;
+      const int kr = idx / (BN / 4), c = colb + (idx % (BN / 4)) * 4;
+      int k = kc0 + kr;
+      k = k < K ? k : K - 1;         // A is zero there; any finite B row does
+      const int cc = c < n4 ? c : 0;  // columns past N: never stored (masked in EPI = 1)
+      breg[i] = *reinterpret_cast<const f4*>(B + static_cast<int64_t>(k) * ldb + cc);
+    }
+  };
+  auto store_chunk = [&](int buf) {
+    if (a_stager) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + rb + 16 * t + 4 * q + r;
-        yl[r] = (labels != nullptr && row < M) ? labels[row] : -1;
-      }
-      // 1) bias, mask, row max
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float m = kNegInf;
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int c = colw + 64 * g + 4 * j + e;
-            float v = acc[t][g][e][r] + bv[g][e];
-            v = c < N ? v : kNegInf;
-            acc[t][g][e][r] = v;
-            m = fmaxf(m, v);
-          }
-        mx[r] = reduce16_max<16>(m);
-      }
-      if (j == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[0][wc][rb + 16 * t + 4 * q + r] = mx[r];
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = rb + 16 * t + 4 * q + r;
-        float m = red[0][0][rr];
-#pragma unroll
-        for (int w = 1; w < WC; ++w) m = fmaxf(m, red[0][w][rr]);
-        mx[r] = m;
-      }
-      __syncthreads();
-      // 2) sum of exp, logit of the label, first index of the max
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float sv = 0.f, x = 0.f;
-        int a = 0x7fffffff;
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int c = colw + 64 * g + 4 * j + e;
-            const float v = acc[t][g][e][r];
-            sv += expf(v - mx[r]);  // exp(-inf) = 0 for masked columns
-            x += (c == yl[r]) ? v : 0.f;
-            a = (v == mx[r] && c < a) ? c : a;
-          }
-        sm[r] = reduce16_sum<16>(sv);
-        xy[r] = reduce16_sum<16>(x);
-        am[r] = reduce16_min<16>(a);
-      }
-      if (j == 0) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int rr = rb + 16 * t + 4 * q + r;
-          red[0][wc][rr] = sm[r];
-          red[1][wc][rr] = xy[r];
-          red[2][wc][rr] = __int_as_float(am[r]);
-        }
-      }
-      __syncthreads();
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int rr = rb + 16 * t + 4 * q + r;
-        float sv = red[0][0][rr], x = red[1][0][rr];
-        int a = __float_as_int(red[2][0][rr]);
-#pragma unroll
-        for (int w = 1; w < WC; ++w) {
-          sv += red[0][w][rr];
-          x += red[1][w][rr];
-          a = min(a, __float_as_int(red[2][w][rr]));
-        }
-        sm[r] = sv;
-        xy[r] = x;
-        am[r] = a;
-      }
-      __syncthreads();  // red is reused by the next tile
-      // 3) outputs
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int64_t row = row0 + rb + 16 * t + 4 * q + r;
-        if (row >= M) continue;
-        const float inv = 1.0f / sm[r];
-        const bool xent = yl[r] >= 0;
-        if (xent && wc == 0 && j == 0) {
-          loss_rows[row] = (mx[r] + logf(sm[r])) - xy[r];  // -log softmax[row, y]
-          if (correct_rows) correct_rows[row] = (am[r] == yl[r]) ? 1.f : 0.f;
-        }
-        if (Cout == nullptr) continue;  // loss / accuracy only (evaluation)
-        float* orow = Cout + row * ldc;
-#pragma unroll
-        for (int g = 0; g < G; ++g) {
-          const int c = colw + 64 * g + 4 * j;
-          if (c >= N) continue;
-          f4 o;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            float p = expf(acc[t][g][e][r] - mx[r]) * inv;
-            if (xent) p = (p - ((c + e) == yl[r] ? 1.f : 0.f)) * scale;
-            o[e] = p;
-          }
-          if (c + 3 < N) {
-            *reinterpret_cast<f4*>(orow + c) = o;
-          } else {
-            orow[c] = o.x;
-            if (c + 1 < N) orow[c + 1] = o.y;
-            if (c + 2 < N) orow[c + 2] = o.z;
-          }
-        }
+      for (int i = 0; i < A4; ++i) {
+        const int idx = tid + AT * i;
+        *reinterpret_cast<f4*>(&As[buf][idx / (KC / 4)][(idx % (KC / 4)) * 4]) = areg[i];
       }
     }
+#pragma unroll
+    for (int i = 0; i < B4; ++i) {
+      const int idx = tid + NT * i;
+      *reinterpret_cast<f4*>(&Bs[buf][idx / (BN / 4)][(idx % (BN / 4)) * 4]) = breg[i];
+    }
+  };
+  auto lds_barrier = [&]() {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  const int arow = wr * 16 + j;
+  const int bl = wc * G * 64 + 4 * j;  // this lane's column inside the LDS B image
+  auto compute_step = [&](int buf, int s) {
+    const f4 af = *reinterpret_cast<const f4*>(&As[buf][arow][s * 16 + 4 * q]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      // all G fragments of this k first (no branch between them: the reads stay in flight
+      // together), then 4G MFMAs; groups past N compute on clamped columns, never stored
+      const float* brow = &Bs[buf][s * 16 + 4 * q + e][bl];
+      f4 bf[G];
+#pragma unroll
+      for (int g = 0; g < G; ++g) bf[g] = *reinterpret_cast<const f4*>(brow + 64 * g);
+#pragma unroll
+      for (int g = 0; g < G; ++g) {
+        acc[0][g][0] = mfma4(af[e], bf[g].x, acc[0][g][0]);
+        acc[0][g][1] = mfma4(af[e], bf[g].y, acc[0][g][1]);
+        acc[0][g][2] = mfma4(af[e], bf[g].z, acc[0][g][2]);
+        acc[0][g][3] = mfma4(af[e], bf[g].w, acc[0][g][3]);
+      }
+    }
+  };
+
+  const int n_chunks = (K + KC - 1) / KC;
+  load_chunk(0);
+  store_chunk(0);
+  lds_barrier();
+  for (int c = 0; c < n_chunks; ++c) {
+    const int k0 = c * KC;
+    const int buf = NB == 2 ? (c & 1) : 0;
+    const bool more = c + 1 < n_chunks;
+    if (more) load_chunk(k0 + KC);  // in flight during this chunk's MFMAs
+    compute_step(buf, 0);
+    if (KC == 32 && k0 + 16 < K) compute_step(buf, 1);
+    if (more) {
+      // two buffers: the other one was last read in chunk c-1, before the barrier that
+      // ended it; one buffer: wait until every wave is done reading this chunk
+      if (NB == 1) lds_barrier();
+      store_chunk(NB == 2 ? buf ^ 1 : 0);
+      lds_barrier();
+    }
   }
+#include "gemm_epilogue.inc"
 }
 
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
@@ -629,6 +611,7 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
 
 struct Shape {
   int RT, G, WR, WC, PF = 1;
+  int BL = 0;  // 1: gemm_bl_kernel (B through LDS; RT = 1, WR = 4)
   int bm() const { return 16 * RT * WR; }
   int bn() const { return 64 * G * WC; }
 };
@@ -641,8 +624,24 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
                        const float* bias, int act, float* C, int64_t ldc, const int32_t* labels,
                        float scale, const float* scale_dev, float* loss_rows,
                        float* correct_rows) {
+#define GCG_GEMM_BL_CASE(g, wc)                                                              \
+  if (s.BL && s.G == g && s.WC == wc) {                                                      \
+    hipLaunchKernelGGL((gemm_bl_kernel<g, wc, EPI>), grid, dim3(256 * (wc)), 0, st, M, N, K, A, \
+                       lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
+                       correct_rows);                                                         \
+    GCG_HIP_CHECK(hipGetLastError());                                                         \
+    return GCG_OK;                                                                            \
+  }
+  GCG_GEMM_BL_CASE(4, 4)
+  GCG_GEMM_BL_CASE(4, 2)
+  GCG_GEMM_BL_CASE(5, 1)
+  GCG_GEMM_BL_CASE(4, 1)
+  GCG_GEMM_BL_CASE(3, 1)
+  GCG_GEMM_BL_CASE(2, 1)
+  GCG_GEMM_BL_CASE(1, 1)
+#undef GCG_GEMM_BL_CASE
 #define GCG_GEMM_CASE(rt, g, wr, wc, pf)                                                    \
-  if (s.RT == rt && s.G == g && s.WR == wr && s.WC == wc && s.PF == pf) {                    \
+  if (!s.BL && s.RT == rt && s.G == g && s.WR == wr && s.WC == wc && s.PF == pf) {           \
     hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI, pf>), grid, dim3(64 * (wr) * (wc)), 0, \
                        st, M, N, K, A,                                                       \
                        lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
@@ -684,6 +683,19 @@ Shape pick_shape(int64_t N, bool fused) {
   //   RT = 2, one B set, 8-wave workgroup              93.1 / 83.8
   // Knobs for experiments: GCG_GEMM_RT=2, GCG_GEMM_8W=1, GCG_GEMM_OCC2=0/1.
   const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
+  // Plain products: B through LDS (gemm_bl_kernel), measured on the train step's shapes
+  // (tools/exp_gemm_bl.py, TFLOP/s, B-from-L2 gemm_kernel -> LDS-B):
+  //   840k x 300 x 930  93.5 -> 96.7 (16 waves x 256 columns)   1.4M x 300 x 930  94.5 -> 97.0
+  //   840k x 930 x 300  90.9 -> 105.1 (4 waves x 320 columns)   1.4M x 930 x 300  91.6 -> 105.7
+  // The fused output layer keeps gemm_kernel: with one LDS-B workgroup per CU its softmax
+  // epilogue and 3 GB of gradient stores do not overlap another workgroup's MFMAs
+  // (77.9-79.3 vs 85.0 TFLOP/s). GCG_GEMM_BL=0 selects gemm_kernel for plain products too.
+  const char* blv = std::getenv("GCG_GEMM_BL");
+  if (!fused && !(blv && std::atoi(blv) == 0)) {
+    if (groups <= 5) return Shape{1, std::max(groups, 1), 4, 1, 0, 1};
+    if (groups <= 8) return Shape{1, 4, 4, 2, 0, 1};
+    return Shape{1, 4, 4, 4, 0, 1};  // 1024 columns per workgroup, grid.y for the rest
+  }
   if (fused || groups > 5) {
     const int g = std::min(4, (groups + 3) / 4);
     if (env_int("GCG_GEMM_8W") && g == 4) return Shape{2, 4, 2, 4, 0};

@@ -225,3 +225,21 @@ def test_side_stream_weight_grads_equal_inline(cuda, shared_w):
     b = _weight_grads(cuda, False, shared_w)
     for x, y in zip(a, b):
         assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 1, 1), (65, 17, 5), (129, 300, 300), (200, 33, 320),
+                                   (257, 64, 321), (130, 300, 512), (300, 300, 930),
+                                   (77, 40, 1024), (100, 20, 1500), (64, 930, 300)])
+def test_lds_b_gemm_equals_register_b_gemm(cuda, M, K, N, monkeypatch):
+    """The plain products' default tiles (B staged through LDS, gemm_bl_kernel) accumulate in
+    the same k order as gemm_kernel (GCG_GEMM_BL=0): bitwise equal, bias + rectify included."""
+    A, B, bias = _rand((M, K), M + 1), _rand((K, N), N + 2), _rand((N,), 3)
+    At = torch.from_numpy(A).to(cuda)
+    Bt = _padded(B, cuda)
+    bt = torch.from_numpy(bias).to(cuda)
+    outs = []
+    for knob in ("1", "0"):
+        monkeypatch.setenv("GCG_GEMM_BL", knob)
+        outs.append((dense.gemm(At, Bt), dense.gemm(At, Bt, bias=bt, act="relu")))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    _check_gemm(outs[0][1].cpu().numpy(), A, B, bias, relu=True)
