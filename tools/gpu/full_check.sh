@@ -13,3 +13,5 @@ for cfg in twitter-us twitter-world; do for order in reference propagate_first; 
 timeout -k 10 300 python -u tools/bench_train.py --config $cfg --order $order > $out/train_${cfg}_${order}.log 2>&1 || { tail -20 $out/train_${cfg}_${order}.log; exit 1; }
 grep '^{' $out/train_${cfg}_${order}.log | python3 -c "import json,sys; r=json.loads(sys.stdin.read()); print(r['config'], r['order'], r['ms_per_step'])"
 done; done
+timeout -k 10 600 python -u bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
+grep '^{' $out/bench.log | cut -c1-700
