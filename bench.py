@@ -294,6 +294,10 @@ def main():
         dist_info = {"exchange": part.exchange, "halo_fraction": round(part.halo_fraction, 4),
                      "exchange_bytes_in_per_gpu": gathered,
                      "exchange_ms": round(t_comm, 4), "local_spmm_ms": round(t_sp, 4),
+                     # the share of the pipelined step not covered by the
+                     # local SpMM (exposed exchange + pipeline fill)
+                     "exposed_comm_ms": round(max(ms - t_sp, 0.0), 4),
+                     "comm_fraction": round(max(ms - t_sp, 0.0) / ms, 4) if ms > 0 else None,
                      "exchange_inbound_GBps_per_gpu": round(gathered / (t_comm * 1e-3) / 1e9, 1),
                      "chunks": args.chunks, "rows_local": part.n_local,
                      "nnz_local": part.nnz_local, "block_rows": part.block_rows,

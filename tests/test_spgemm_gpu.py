@@ -75,3 +75,38 @@ def test_spgemm_empty(cuda):
     assert C.nnz == 0 and C.to_scipy().shape == (5, 3)
     with pytest.raises(ValueError):
         gs.spgemm(gs.DeviceCSR.from_scipy(B, cuda), gs.DeviceCSR.from_scipy(B, cuda))
+
+
+@pytest.mark.parametrize("chunk", [1, 37, 1000, 50_000])
+def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
+    """Row-chunked expand-sort-reduce (products > int32 at Twitter-World scale): forcing tiny
+    chunks -- single rows larger than a chunk, chunks of empty rows -- leaves C bitwise equal."""
+    monkeypatch.setenv("GCG_SPGEMM_CHUNK", str(chunk))
+    rng = np.random.default_rng(chunk)
+    A = sps.random(900, 400, density=0.03, random_state=3, format="lil", dtype=np.float32)
+    A[100:220, :] = 0          # a block of empty rows
+    A[5, :] = 1.0              # one dense row (400 * ~15 products)
+    A = sps.csr_matrix(A)
+    A.data = rng.standard_normal(A.nnz).astype(np.float32)
+    B = sps.random(400, 250, density=0.04, random_state=4, format="lil", dtype=np.float32)
+    B[7:30, :] = 0             # rows of A pointing at empty rows of B
+    B = sps.csr_matrix(B)
+    B.data = rng.standard_normal(B.nnz).astype(np.float32)
+    # exact cancellations: column 0 of C gets +x and -x from two rows of B
+    B = sps.lil_matrix(B)
+    B[1, 0], B[2, 0] = 1.0, -1.0
+    B = sps.csr_matrix(B)
+    A = sps.lil_matrix(A)
+    A[600, 1], A[600, 2] = 2.0, 2.0
+    A = sps.csr_matrix(A)
+    C = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
+    ref = canon(A @ B)
+    assert np.array_equal(C.indptr, ref.indptr)
+    assert np.array_equal(C.indices, ref.indices)
+    assert np.array_equal(C.data, ref.data)
+    A64 = torch.as_tensor(A.data.astype(np.float64) * 1.0000001, device=cuda)
+    C64 = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda), a_data64=A64).to_scipy()
+    A64h = sps.csr_matrix((A64.cpu().numpy(), A.indices, A.indptr), shape=A.shape)
+    ref64 = canon((A64h @ B.astype(np.float64)).astype(np.float32))
+    assert np.array_equal(C64.indptr, ref64.indptr) and np.array_equal(C64.indices, ref64.indices)
+    assert np.array_equal(C64.data, ref64.data)
