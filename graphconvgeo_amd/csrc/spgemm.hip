@@ -124,6 +124,354 @@ struct DevBuf {
   ~DevBuf() { if (p) (void)hipFreeAsync(p, s); }
 };
 
+
+// ---- row-wise SpGEMM with a dense LDS accumulator (the default for p <= 8 slabs) ---------
+// One 1024-thread workgroup per row of C, rows dispatched longest-first. The row's products
+// are staged through LDS in traversal order (A row storage order, then B row order), NB at a
+// time, and added into a dense LDS accumulator that covers a slab of `sw` output columns.
+// OWN = 4 owner waves apply them: wave w adds exactly the columns c with c % 4 == w and walks
+// the steps (nonzeros of the A row) in order, so every C entry receives its products in
+// scipy csr_matmat's order (sums[k] += v * Bx[kk], from 0) without atomics; inside one step
+// the columns are distinct (a CSR row), so the lanes of a wave never collide. Extraction
+// walks the slab in column order (canonical output), keeps sums != 0 (scipy's
+// `if (sums[head] != 0)`) and re-zeroes the slab. Output goes to an upper-bound layout
+// (row i at rowoff[i], its product count prefix) and is compacted afterwards.
+constexpr int kRowsNT = 1024;
+constexpr int kRowsNB = 2048;
+
+template <int NW>
+__device__ __forceinline__ int block_excl_scan(int v, int* s_wsum, int& total) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int x = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int y = __shfl_up(x, o, 64);
+    if (lane >= o) x += y;
+  }
+  if (lane == 63) s_wsum[wave] = x;
+  __syncthreads();
+  int wpre = 0;
+  total = 0;
+#pragma unroll
+  for (int w = 0; w < NW; ++w) {
+    const int s = s_wsum[w];
+    wpre += w < wave ? s : 0;
+    total += s;
+  }
+  __syncthreads();  // s_wsum reusable
+  return wpre + x - v;
+}
+
+template <typename TA, typename TACC, int SMAX>
+__global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
+    int64_t p, int sw, const int32_t* __restrict__ order, const int32_t* __restrict__ a_ptr,
+    const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr,
+    const int32_t* __restrict__ b_idx, const float* __restrict__ b_val, const int64_t* __restrict__ rowoff,
+    int32_t* __restrict__ t_idx, float* __restrict__ t_val, int64_t* __restrict__ kept) {
+  constexpr int NT = kRowsNT, NB = kRowsNB, NW = NT / 64, OWN = 4;
+  __shared__ TACC acc[SMAX];
+  __shared__ int32_t s_col[NB];
+  __shared__ TACC s_val[NB];
+  __shared__ int32_t s_pref[NT + 1];
+  __shared__ int32_t s_bst[NT];
+  __shared__ TACC s_av[NT];
+  __shared__ int32_t s_wsum[NW];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6;
+  for (int k = t; k < SMAX; k += NT) acc[k] = TACC(0);
+  const int64_t row = order[blockIdx.x];
+  const int32_t a0 = a_ptr[row], a1 = a_ptr[row + 1];
+  const int64_t out0 = rowoff[row];
+  const int n_slabs = static_cast<int>((p + sw - 1) / sw);
+  const int spt = sw / NT;  // columns per thread in the extraction
+  int base = 0;             // outputs of this row so far (block-uniform)
+  __syncthreads();
+  for (int sl = 0; sl < n_slabs; ++sl) {
+    const int64_t c0 = static_cast<int64_t>(sl) * sw;
+    const int64_t c1 = min(p, c0 + sw);
+    for (int32_t jb = a0; jb < a1; jb += NT) {
+      const int ns = min(NT, a1 - jb);
+      int len = 0;
+      if (t < ns) {
+        const int32_t r = a_idx[jb + t];
+        const int32_t b0 = b_ptr[r];
+        len = b_ptr[r + 1] - b0;
+        s_bst[t] = b0;
+        s_av[t] = static_cast<TACC>(a_val[jb + t]);
+      }
+      int total;
+      const int excl = block_excl_scan<NW>(len, s_wsum, total);
+      s_pref[t] = excl;
+      if (t == 0) s_pref[NT] = total;
+      __syncthreads();
+      for (int w0 = 0; w0 < total; w0 += NB) {
+        const int wn = min(NB, total - w0);
+        for (int q = t; q < wn; q += NT) {  // stage positions [w0, w0 + wn)
+          const int pos = w0 + q;
+          int lo = 0, hi = ns - 1;  // the step holding pos: last j with s_pref[j] <= pos
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pref[mid] <= pos) lo = mid; else hi = mid - 1;
+          }
+          const int32_t kk = s_bst[lo] + (pos - s_pref[lo]);
+          s_col[q] = b_idx[kk];
+          s_val[q] = s_av[lo] * static_cast<TACC>(b_val[kk]);
+        }
+        __syncthreads();
+        if (wave < OWN) {
+          int lo = 0, hi = ns - 1;  // first step overlapping the window
+          while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (s_pref[mid] <= w0) lo = mid; else hi = mid - 1;
+          }
+          for (int j = lo; j < ns && s_pref[j] < w0 + wn; ++j) {
+            const int e0 = max(s_pref[j], w0) - w0, e1 = min(s_pref[j + 1], w0 + wn) - w0;
+            for (int e = e0 + lane; e < e1; e += 64) {
+              const int c = s_col[e];
+              if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) acc[c - c0] = acc[c - c0] + s_val[e];
+            }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    // extraction of the slab, column order; re-zeroes it
+    const int k0 = t * spt;
+    const int kn = static_cast<int>(min<int64_t>(spt, max<int64_t>(0, c1 - c0 - k0)));
+    int cnt = 0;
+    for (int i = 0; i < kn; ++i) cnt += acc[k0 + i] != TACC(0) ? 1 : 0;
+    int total;
+    int o = base + block_excl_scan<NW>(cnt, s_wsum, total);
+    for (int i = 0; i < kn; ++i) {
+      const TACC v = acc[k0 + i];
+      if (v != TACC(0)) {
+        t_idx[out0 + o] = static_cast<int32_t>(c0 + k0 + i);
+        t_val[out0 + o] = static_cast<float>(v);
+        ++o;
+        acc[k0 + i] = TACC(0);
+      }
+    }
+    base += total;
+    __syncthreads();
+  }
+  if (t == 0) kept[row] = base;
+}
+
+
+// Rows with at most kSmallSteps nonzeros and kSmallProducts products skip the slabs: the
+// workgroup stages the row's products (key = column << 11 | traversal position), bitonic-sorts
+// the keys in LDS, and sums every run of equal columns in position order -- the same
+// csr_matmat order, independent of the number of output columns. 256 threads, ~21 KB of LDS
+// (several workgroups per CU); the bulk of a power-law graph's rows.
+constexpr int kSmallNT = 256;
+constexpr int kSmallSteps = kSmallNT;
+constexpr int kSmallProducts = 2048;  // positions fit 11 bits of the sort key
+constexpr int64_t kSmallMaxCols = int64_t{1} << 20;  // column < 2^21: keys stay below the pad key
+
+template <typename TA, typename TACC>
+__global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
+    const int32_t* __restrict__ order, const int32_t* __restrict__ a_ptr, const int32_t* __restrict__ a_idx,
+    const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr, const int32_t* __restrict__ b_idx,
+    const float* __restrict__ b_val, const int64_t* __restrict__ rowoff, int32_t* __restrict__ t_idx,
+    float* __restrict__ t_val, int64_t* __restrict__ kept) {
+  constexpr int NT = kSmallNT, NB = kSmallProducts, NW = NT / 64;
+  __shared__ uint32_t s_key[NB];
+  __shared__ TACC s_val[NB];
+  __shared__ int32_t s_pref[NT + 1];
+  __shared__ int32_t s_bst[NT];
+  __shared__ TACC s_av[NT];
+  __shared__ int32_t s_wsum[NW];
+  const int t = threadIdx.x;
+  const int64_t row = order[blockIdx.x];
+  const int32_t a0 = a_ptr[row];
+  const int ns = a_ptr[row + 1] - a0;  // <= NT (host-side classification)
+  int len = 0;
+  if (t < ns) {
+    const int32_t r = a_idx[a0 + t];
+    const int32_t b0 = b_ptr[r];
+    len = b_ptr[r + 1] - b0;
+    s_bst[t] = b0;
+    s_av[t] = static_cast<TACC>(a_val[a0 + t]);
+  }
+  int total;
+  const int excl = block_excl_scan<NW>(len, s_wsum, total);  // total <= NB
+  s_pref[t] = excl;
+  int sz = 64;
+  while (sz < total) sz <<= 1;
+  __syncthreads();
+  for (int q = t; q < sz; q += NT) {
+    uint32_t key = 0xffffffffu;
+    if (q < total) {
+      int lo = 0, hi = ns - 1;
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_pref[mid] <= q) lo = mid; else hi = mid - 1;
+      }
+      const int32_t kk = s_bst[lo] + (q - s_pref[lo]);
+      key = (static_cast<uint32_t>(b_idx[kk]) << 11) | static_cast<uint32_t>(q);
+      s_val[q] = s_av[lo] * static_cast<TACC>(b_val[kk]);
+    }
+    s_key[q] = key;
+  }
+  __syncthreads();
+  for (int k = 2; k <= sz; k <<= 1) {  // bitonic sort, ascending; keys are unique
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = t; i < sz; i += NT) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint32_t x = s_key[i], y = s_key[ixj];
+          if ((x > y) == ((i & k) == 0)) {
+            s_key[i] = y;
+            s_key[ixj] = x;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // runs of equal columns: thread t owns sorted positions [t*per, (t+1)*per) and sums the
+  // runs that START there, in position order
+  const int per = (total + NT - 1) / NT;
+  const int s0 = min(total, t * per), s1 = min(total, s0 + per);
+  int cnt = 0;
+  for (int s = s0; s < s1; ++s) {
+    const uint32_t col = s_key[s] >> 11;
+    if (s > 0 && (s_key[s - 1] >> 11) == col) continue;
+    TACC acc = TACC(0);
+    for (int u = s; u < total && (s_key[u] >> 11) == col; ++u) acc = acc + s_val[s_key[u] & 2047u];
+    cnt += acc != TACC(0) ? 1 : 0;
+  }
+  int n_kept;
+  int o = block_excl_scan<NW>(cnt, s_wsum, n_kept);
+  const int64_t out0 = rowoff[row];
+  for (int s = s0; s < s1; ++s) {
+    const uint32_t col = s_key[s] >> 11;
+    if (s > 0 && (s_key[s - 1] >> 11) == col) continue;
+    TACC acc = TACC(0);
+    for (int u = s; u < total && (s_key[u] >> 11) == col; ++u) acc = acc + s_val[s_key[u] & 2047u];
+    if (acc != TACC(0)) {
+      t_idx[out0 + o] = static_cast<int32_t>(col);
+      t_val[out0 + o] = static_cast<float>(acc);
+      ++o;
+    }
+  }
+  if (t == 0) kept[row] = n_kept;
+}
+
+// C rows from the upper-bound layout: row i's kept entries at rowoff[i] -> c_ptr[i]. One wave
+// per row.
+__global__ void spgemm_compact_kernel(int64_t m, const int64_t* __restrict__ rowoff,
+                                      const int64_t* __restrict__ cptr64, const int32_t* __restrict__ t_idx,
+                                      const float* __restrict__ t_val, int32_t* __restrict__ c_ptr,
+                                      int32_t* __restrict__ c_idx, float* __restrict__ c_val) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (blockDim.x / 64);
+  for (int64_t r = static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); r <= m; r += waves) {
+    const int64_t d = cptr64[r];
+    if (lane == 0) c_ptr[r] = static_cast<int32_t>(d);
+    if (r == m) continue;
+    const int64_t s = rowoff[r], n = cptr64[r + 1] - d;
+    for (int64_t k = lane; k < n; k += 64) {
+      c_idx[d + k] = t_idx[s + k];
+      c_val[d + k] = t_val[s + k];
+    }
+  }
+}
+
+// Row products (clamped to int32) for the longest-first order.
+// Rows that the small-row kernel cannot take (more than kSmallSteps nonzeros) are keyed
+// above kSmallProducts so they sort into the dense-slab set.
+__global__ void row_products_u32_kernel(int64_t m, const int64_t* __restrict__ rowoff,
+                                        const int32_t* __restrict__ a_ptr, int small_ok,
+                                        uint32_t* __restrict__ key, int32_t* __restrict__ id) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < m; i += stride) {
+    int64_t v = rowoff[i + 1] - rowoff[i];
+    if (v <= kSmallProducts && (!small_ok || a_ptr[i + 1] - a_ptr[i] > kSmallSteps)) v = kSmallProducts + 1;
+    key[i] = static_cast<uint32_t>(v > 0xffffffffLL ? 0xffffffffLL : v);
+    id[i] = static_cast<int32_t>(i);
+  }
+}
+
+template <typename TACC> struct RowsSlab;
+template <> struct RowsSlab<float> { static constexpr int kMax = 25 * kRowsNT; };   // 100 KB
+template <> struct RowsSlab<double> { static constexpr int kMax = 13 * kRowsNT; };  // 104 KB
+constexpr int kRowsMaxSlabs = 8;
+
+template <typename TA, typename TACC>
+gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
+                       const TA* a_val, const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
+                       int64_t n_products, const int64_t* rowoff_dev, int32_t* c_ptr, int32_t* c_idx,
+                       float* c_val, int64_t* nnz_c_dev, hipStream_t st) {
+  (void)nnz_a;
+  constexpr int SMAX = RowsSlab<TACC>::kMax;
+  const int64_t n_slabs = (p + SMAX - 1) / SMAX;
+  int64_t sw = (p + n_slabs - 1) / n_slabs;
+  sw = std::max<int64_t>(kRowsNT, (sw + kRowsNT - 1) / kRowsNT * kRowsNT);
+  DevBuf b_key, b_key2, b_id, b_id2, b_tidx, b_tval, b_kept, b_cp64, b_tmp;
+  size_t t_sort = 0, t_scan = 0;
+  {
+    uint32_t* k = nullptr; int32_t* v = nullptr; int64_t* o = nullptr;
+    if (hipcub::DeviceRadixSort::SortPairsDescending(nullptr, t_sort, k, k, v, v, static_cast<int>(m)) != hipSuccess ||
+        hipcub::DeviceScan::ExclusiveSum(nullptr, t_scan, o, o, static_cast<int>(m + 1)) != hipSuccess)
+      return fail(GCG_ERR_HIP, "hipcub sizing failed");
+  }
+  auto alloc = [&](DevBuf& b, size_t bytes) -> hipError_t {
+    b.s = st;
+    return hipMallocAsync(&b.p, std::max<size_t>(bytes, 16), st);
+  };
+  hipError_t e = alloc(b_key, m * sizeof(uint32_t));
+  if (e == hipSuccess) e = alloc(b_key2, m * sizeof(uint32_t));
+  if (e == hipSuccess) e = alloc(b_id, m * sizeof(int32_t));
+  if (e == hipSuccess) e = alloc(b_id2, m * sizeof(int32_t));
+  if (e == hipSuccess) e = alloc(b_tidx, n_products * sizeof(int32_t));
+  if (e == hipSuccess) e = alloc(b_tval, n_products * sizeof(float));
+  if (e == hipSuccess) e = alloc(b_kept, (m + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = alloc(b_cp64, (m + 1) * sizeof(int64_t));
+  if (e == hipSuccess) e = alloc(b_tmp, std::max(t_sort, t_scan));
+  if (e != hipSuccess) return fail(GCG_ERR_ALLOC, "SpGEMM row temporaries: %s", hipGetErrorString(e));
+  auto* key = static_cast<uint32_t*>(b_key.p);
+  auto* key2 = static_cast<uint32_t*>(b_key2.p);
+  auto* id = static_cast<int32_t*>(b_id.p);
+  auto* id2 = static_cast<int32_t*>(b_id2.p);
+  auto* kept = static_cast<int64_t*>(b_kept.p);
+  auto* cp64 = static_cast<int64_t*>(b_cp64.p);
+  const int small_ok = (p <= kSmallMaxCols && env_int("GCG_SPGEMM_NO_SMALL") == 0) ? 1 : 0;
+  hipLaunchKernelGGL(row_products_u32_kernel, dim3(grid_for(m)), dim3(256), 0, st, m, rowoff_dev, a_ptr, small_ok,
+                     key, id);
+  GCG_HIP_CHECK(hipGetLastError());
+  size_t tb = t_sort;
+  GCG_HIP_CHECK(hipcub::DeviceRadixSort::SortPairsDescending(b_tmp.p, tb, key, key2, id, id2, static_cast<int>(m), 0, 32, st));
+  GCG_HIP_CHECK(hipMemsetAsync(kept + m, 0, sizeof(int64_t), st));
+  // rows [0, n_big) of the longest-first order take the dense slabs, the rest the sort kernel
+  std::vector<uint32_t> skey(m);
+  GCG_HIP_CHECK(hipMemcpyAsync(skey.data(), key2, m * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+  GCG_HIP_CHECK(hipStreamSynchronize(st));
+  const int64_t n_big = std::lower_bound(skey.begin(), skey.end(), static_cast<uint32_t>(kSmallProducts),
+                                         [](uint32_t a, uint32_t b) { return a > b; }) - skey.begin();
+  auto* tidx = static_cast<int32_t*>(b_tidx.p);
+  auto* tval = static_cast<float*>(b_tval.p);
+  if (n_big > 0)
+    hipLaunchKernelGGL((spgemm_rows_kernel<TA, TACC, SMAX>), dim3(static_cast<unsigned>(n_big)), dim3(kRowsNT), 0, st,
+                       p, static_cast<int>(sw), id2, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
+                       tval, kept);
+  if (m - n_big > 0)
+    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>), dim3(static_cast<unsigned>(m - n_big)), dim3(kSmallNT),
+                       0, st, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx, tval, kept);
+  GCG_HIP_CHECK(hipGetLastError());
+  tb = t_scan;
+  GCG_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(b_tmp.p, tb, kept, cp64, static_cast<int>(m + 1), st));
+  int64_t nnz_c = 0;
+  GCG_HIP_CHECK(hipMemcpyAsync(&nnz_c, cp64 + m, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  GCG_HIP_CHECK(hipStreamSynchronize(st));
+  if (nnz_c > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "nnz(C) = %lld exceeds int32 CSR", (long long)nnz_c);
+  hipLaunchKernelGGL(spgemm_compact_kernel, dim3(grid_for(m * 64)), dim3(256), 0, st, m, rowoff_dev, cp64,
+                     static_cast<const int32_t*>(b_tidx.p), static_cast<const float*>(b_tval.p), c_ptr, c_idx, c_val);
+  GCG_HIP_CHECK(hipGetLastError());
+  GCG_HIP_CHECK(hipMemcpyAsync(nnz_c_dev, cp64 + m, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
+  GCG_HIP_CHECK(hipStreamSynchronize(st));  // temporaries are freed stream-ordered on return
+  return GCG_OK;
+}
+
 // Products per row chunk: the expand-sort-reduce temporaries are ~40 B per product, so a
 // chunk of 2^29 products holds ~21 GB of HBM; row chunks also keep every hipcub item count
 // and the int32 permutation within range. Twitter-World H.X (2.65e9 products) -> 5 chunks.
@@ -181,6 +529,10 @@ gcg_status spgemm_impl(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int
   if (rowoff[m] != n_products)
     return fail(GCG_ERR_INVALID_ARG, "n_products %lld != %lld (from gcg_spgemm_products)",
                 (long long)n_products, (long long)rowoff[m]);
+  if (m <= INT32_MAX && (p + RowsSlab<TACC>::kMax - 1) / RowsSlab<TACC>::kMax <= kRowsMaxSlabs &&
+      env_int("GCG_SPGEMM_ESC") == 0)
+    return spgemm_rows<TA, TACC>(m, p, nnz_a, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, n_products, rowoff_dev,
+                                 c_ptr, c_idx, c_val, nnz_c_dev, st);
   const int64_t kChunkProducts = chunk_products();
   std::vector<int64_t> cuts{0};  // greedy row chunks of <= kChunkProducts products (>= 1 row)
   while (cuts.back() < m) {

@@ -81,6 +81,7 @@ def test_spgemm_empty(cuda):
 def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
     """Row-chunked expand-sort-reduce (products > int32 at Twitter-World scale): forcing tiny
     chunks -- single rows larger than a chunk, chunks of empty rows -- leaves C bitwise equal."""
+    monkeypatch.setenv("GCG_SPGEMM_ESC", "1")  # the expand-sort-reduce path
     monkeypatch.setenv("GCG_SPGEMM_CHUNK", str(chunk))
     rng = np.random.default_rng(chunk)
     A = sps.random(900, 400, density=0.03, random_state=3, format="lil", dtype=np.float32)
@@ -110,3 +111,52 @@ def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
     ref64 = canon((A64h @ B.astype(np.float64)).astype(np.float32))
     assert np.array_equal(C64.indptr, ref64.indptr) and np.array_equal(C64.indices, ref64.indices)
     assert np.array_equal(C64.data, ref64.data)
+
+
+@pytest.mark.parametrize("path", ["rows", "dense", "esc"])
+@pytest.mark.parametrize("p", [300, 30_000, 60_000])
+def test_spgemm_rows_kernel_shapes(cuda, monkeypatch, path, p):
+    """The row-wise kernels (small rows: LDS sort; large rows: dense LDS slabs) across their regimes: several column slabs
+    (p > 25,600 f32 / 13,312 f64), rows with > 2,048 products (several staging windows) and
+    > 1,024 nonzeros (several step blocks), B rows longer than a wave, empty rows of A and B,
+    exact cancellations -- bitwise scipy, f32 and f64 accumulation, both SpGEMM paths."""
+    monkeypatch.setenv("GCG_SPGEMM_ESC", "1" if path == "esc" else "0")
+    monkeypatch.setenv("GCG_SPGEMM_NO_SMALL", "1" if path == "dense" else "0")  # every row on slabs
+    rng = np.random.default_rng(p)
+    m, n = 400, 3000
+    A = sps.random(m, n, density=0.004, random_state=5, format="lil", dtype=np.float32)
+    A[3, :] = 1.0                         # 3,000 nonzeros: 3 step blocks
+    A[10, :1500] = 1.0
+    A[50:80, :] = 0                       # empty rows
+    A = sps.csr_matrix(A)
+    A.data = rng.standard_normal(A.nnz).astype(np.float32)
+    nnz_row = rng.integers(0, 200, n)     # B rows of 0..199 entries (several lanes rounds)
+    nnz_row[:40] = 0
+    rows = np.repeat(np.arange(n), nnz_row)
+    cols = np.concatenate([rng.choice(p, k, replace=False) for k in nnz_row])
+    B = sps.csr_matrix((rng.standard_normal(rows.size).astype(np.float32), (rows, cols)), shape=(n, p))
+    B.sort_indices()
+    # cancellation: C[7, c] = x - x
+    B = sps.lil_matrix(B)
+    B[1000, p - 1], B[1001, p - 1] = 3.0, -3.0
+    B = sps.csr_matrix(B)
+    A = sps.lil_matrix(A)
+    A[7, :] = 0
+    A[7, 1000], A[7, 1001] = 0.5, 0.5
+    A = sps.csr_matrix(A)
+    Ad, Bd = gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)
+    C = gs.spgemm(Ad, Bd).to_scipy()
+    ref = canon(A @ B)
+    assert C[7, p - 1] == 0 and ref[7, p - 1] == 0
+    assert np.array_equal(C.indptr, ref.indptr)
+    assert np.array_equal(C.indices, ref.indices)
+    assert np.array_equal(C.data, ref.data)
+    a64 = torch.as_tensor(A.data.astype(np.float64) / 3.0, device=cuda)
+    C64 = gs.spgemm(Ad, Bd, a_data64=a64).to_scipy()
+    A64 = sps.csr_matrix((a64.cpu().numpy(), A.indices, A.indptr), shape=A.shape)
+    ref64 = canon((A64 @ B.astype(np.float64)).astype(np.float32))
+    assert np.array_equal(C64.indptr, ref64.indptr) and np.array_equal(C64.indices, ref64.indices)
+    assert np.array_equal(C64.data, ref64.data)
+    Cacc = gs.spgemm(Ad, Bd, accumulate_f64=True).to_scipy()  # f32 A, float64 sums
+    refacc = canon((A.astype(np.float64) @ B.astype(np.float64)).astype(np.float32))
+    assert np.array_equal(Cacc.indices, refacc.indices) and np.array_equal(Cacc.data, refacc.data)
