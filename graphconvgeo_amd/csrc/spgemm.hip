@@ -205,29 +205,45 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
       __syncthreads();
       for (int w0 = 0; w0 < total; w0 += NB) {
         const int wn = min(NB, total - w0);
-        for (int q = t; q < wn; q += NT) {  // stage positions [w0, w0 + wn)
-          const int pos = w0 + q;
-          int lo = 0, hi = ns - 1;  // the step holding pos: last j with s_pref[j] <= pos
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pref[mid] <= pos) lo = mid; else hi = mid - 1;
+        int jlo = 0, hi = ns - 1;  // first step overlapping the window: last j with s_pref[j] <= w0
+        while (jlo < hi) {
+          const int mid = (jlo + hi + 1) >> 1;
+          if (s_pref[mid] <= w0) jlo = mid; else hi = mid - 1;
+        }
+        // stage positions [w0, w0 + wn): wave w copies steps jlo + w, jlo + w + NW, ... (one
+        // coalesced B-row read per step)
+        for (int j = jlo + wave; j < ns && s_pref[j] < w0 + wn; j += NW) {
+          const int e0 = max(s_pref[j], w0), e1 = min(s_pref[j + 1], w0 + wn);
+          const int32_t kb = s_bst[j] - s_pref[j];
+          const TACC av = s_av[j];
+          for (int pos = e0 + lane; pos < e1; pos += 64) {
+            s_col[pos - w0] = b_idx[kb + pos];
+            s_val[pos - w0] = av * static_cast<TACC>(b_val[kb + pos]);
           }
-          const int32_t kk = s_bst[lo] + (pos - s_pref[lo]);
-          s_col[q] = b_idx[kk];
-          s_val[q] = s_av[lo] * static_cast<TACC>(b_val[kk]);
         }
         __syncthreads();
         if (wave < OWN) {
-          int lo = 0, hi = ns - 1;  // first step overlapping the window
-          while (lo < hi) {
-            const int mid = (lo + hi + 1) >> 1;
-            if (s_pref[mid] <= w0) lo = mid; else hi = mid - 1;
+          // steps [jlo, jhi) overlap the window; their bounds go through VGPRs (readlane) in
+          // blocks of 64 so the only LDS traffic per step is the entries themselves. The adds
+          // are LDS atomics without return: a wave's LDS operations execute in program order,
+          // so entry (j, c) is added after every (j' < j, c) with no wait on the accumulator;
+          // inside one step the columns are distinct.
+          int jhi = jlo, hj = ns;  // first step starting at or after w0 + wn
+          while (jhi < hj) {
+            const int mid = (jhi + hj) >> 1;
+            if (s_pref[mid] < w0 + wn) jhi = mid + 1; else hj = mid;
           }
-          for (int j = lo; j < ns && s_pref[j] < w0 + wn; ++j) {
-            const int e0 = max(s_pref[j], w0) - w0, e1 = min(s_pref[j + 1], w0 + wn) - w0;
-            for (int e = e0 + lane; e < e1; e += 64) {
-              const int c = s_col[e];
-              if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) acc[c - c0] = acc[c - c0] + s_val[e];
+          for (int jb2 = jlo; jb2 < jhi; jb2 += 64) {
+            const int nj = min(64, jhi - jb2);
+            const int p0 = lane < nj ? s_pref[jb2 + lane] : 0;
+            const int p1 = lane < nj ? s_pref[jb2 + lane + 1] : 0;
+            for (int q = 0; q < nj; ++q) {
+              const int e0 = max(__builtin_amdgcn_readlane(p0, q), w0) - w0;
+              const int e1 = min(__builtin_amdgcn_readlane(p1, q), w0 + wn) - w0;
+              for (int e = e0 + lane; e < e1; e += 64) {
+                const int c = s_col[e];
+                if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) atomicAdd(&acc[c - c0], s_val[e]);
+              }
             }
           }
         }
@@ -450,14 +466,36 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
                                          [](uint32_t a, uint32_t b) { return a > b; }) - skey.begin();
   auto* tidx = static_cast<int32_t*>(b_tidx.p);
   auto* tval = static_cast<float*>(b_tval.p);
+  // The two row sets are independent: the small-row kernel (~20-29 KB of LDS) runs on a side
+  // stream so its workgroups fill the LDS a dense-slab workgroup (131-148 KB) leaves free.
+  hipStream_t side = nullptr;
+  hipEvent_t ev_ready = nullptr, ev_small = nullptr;
+  const bool both = n_big > 0 && m - n_big > 0;
+  if (both) {
+    GCG_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+    GCG_HIP_CHECK(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
+    GCG_HIP_CHECK(hipEventCreateWithFlags(&ev_small, hipEventDisableTiming));
+    GCG_HIP_CHECK(hipEventRecord(ev_ready, st));
+    GCG_HIP_CHECK(hipStreamWaitEvent(side, ev_ready, 0));
+  }
+  hipStream_t st_small = both ? side : st;
+  if (m - n_big > 0)
+    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>), dim3(static_cast<unsigned>(m - n_big)), dim3(kSmallNT),
+                       0, st_small, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx, tval,
+                       kept);
   if (n_big > 0)
     hipLaunchKernelGGL((spgemm_rows_kernel<TA, TACC, SMAX>), dim3(static_cast<unsigned>(n_big)), dim3(kRowsNT), 0, st,
                        p, static_cast<int>(sw), id2, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
                        tval, kept);
-  if (m - n_big > 0)
-    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>), dim3(static_cast<unsigned>(m - n_big)), dim3(kSmallNT),
-                       0, st, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx, tval, kept);
-  GCG_HIP_CHECK(hipGetLastError());
+  const hipError_t launch_err = hipGetLastError();
+  if (both) {
+    (void)hipEventRecord(ev_small, side);
+    (void)hipStreamWaitEvent(st, ev_small, 0);
+    (void)hipEventDestroy(ev_ready);
+    (void)hipEventDestroy(ev_small);
+    (void)hipStreamDestroy(side);  // returns at once; the queued work completes
+  }
+  if (launch_err != hipSuccess) return fail(GCG_ERR_HIP, "SpGEMM row kernels: %s", hipGetErrorString(launch_err));
   tb = t_scan;
   GCG_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(b_tmp.p, tb, kept, cp64, static_cast<int>(m + 1), st));
   int64_t nnz_c = 0;
