@@ -168,10 +168,12 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
     const int32_t* __restrict__ a_idx, const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr,
     const int32_t* __restrict__ b_idx, const float* __restrict__ b_val, const int64_t* __restrict__ rowoff,
     int32_t* __restrict__ t_idx, float* __restrict__ t_val, int64_t* __restrict__ kept) {
-  constexpr int NT = kRowsNT, NB = kRowsNB, NW = NT / 64, OWN = 4;
+  // NB products per staging buffer, two buffers: waves OWN.. stage window w+1 while the
+  // owner waves apply window w
+  constexpr int NT = kRowsNT, NB = sizeof(TACC) == 8 ? kRowsNB / 2 : kRowsNB, NW = NT / 64, OWN = 4;
   __shared__ TACC acc[SMAX];
-  __shared__ int32_t s_col[NB];
-  __shared__ TACC s_val[NB];
+  __shared__ int32_t s_col[2][NB];
+  __shared__ TACC s_val[2][NB];
   __shared__ int32_t s_pref[NT + 1];
   __shared__ int32_t s_bst[NT];
   __shared__ TACC s_av[NT];
@@ -203,50 +205,64 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
       s_pref[t] = excl;
       if (t == 0) s_pref[NT] = total;
       __syncthreads();
-      for (int w0 = 0; w0 < total; w0 += NB) {
-        const int wn = min(NB, total - w0);
-        int jlo = 0, hi = ns - 1;  // first step overlapping the window: last j with s_pref[j] <= w0
-        while (jlo < hi) {
-          const int mid = (jlo + hi + 1) >> 1;
-          if (s_pref[mid] <= w0) jlo = mid; else hi = mid - 1;
+      // first step overlapping the window starting at w0: last j with s_pref[j] <= w0
+      auto first_step = [&](int w0) {
+        int lo = 0, hi = ns - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_pref[mid] <= w0) lo = mid; else hi = mid - 1;
         }
-        // stage positions [w0, w0 + wn): wave w copies steps jlo + w, jlo + w + NW, ... (one
-        // coalesced B-row read per step)
-        for (int j = jlo + wave; j < ns && s_pref[j] < w0 + wn; j += NW) {
+        return lo;
+      };
+      // stage positions [w0, w0 + wn) into buffer `buf`: stager wave v of nv copies steps
+      // jlo + v, jlo + v + nv, ... (one coalesced B-row read per step)
+      auto stage = [&](int buf, int w0, int v, int nv) {
+        const int wn = min(NB, total - w0);
+        for (int j = first_step(w0) + v; j < ns && s_pref[j] < w0 + wn; j += nv) {
           const int e0 = max(s_pref[j], w0), e1 = min(s_pref[j + 1], w0 + wn);
           const int32_t kb = s_bst[j] - s_pref[j];
           const TACC av = s_av[j];
           for (int pos = e0 + lane; pos < e1; pos += 64) {
-            s_col[pos - w0] = b_idx[kb + pos];
-            s_val[pos - w0] = av * static_cast<TACC>(b_val[kb + pos]);
+            s_col[buf][pos - w0] = b_idx[kb + pos];
+            s_val[buf][pos - w0] = av * static_cast<TACC>(b_val[kb + pos]);
           }
         }
-        __syncthreads();
-        if (wave < OWN) {
-          // steps [jlo, jhi) overlap the window; their bounds go through VGPRs (readlane) in
-          // blocks of 64 so the only LDS traffic per step is the entries themselves. The adds
-          // are LDS atomics without return: a wave's LDS operations execute in program order,
-          // so entry (j, c) is added after every (j' < j, c) with no wait on the accumulator;
-          // inside one step the columns are distinct.
-          int jhi = jlo, hj = ns;  // first step starting at or after w0 + wn
-          while (jhi < hj) {
-            const int mid = (jhi + hj) >> 1;
-            if (s_pref[mid] < w0 + wn) jhi = mid + 1; else hj = mid;
-          }
-          for (int jb2 = jlo; jb2 < jhi; jb2 += 64) {
-            const int nj = min(64, jhi - jb2);
-            const int p0 = lane < nj ? s_pref[jb2 + lane] : 0;
-            const int p1 = lane < nj ? s_pref[jb2 + lane + 1] : 0;
-            for (int q = 0; q < nj; ++q) {
-              const int e0 = max(__builtin_amdgcn_readlane(p0, q), w0) - w0;
-              const int e1 = min(__builtin_amdgcn_readlane(p1, q), w0 + wn) - w0;
-              for (int e = e0 + lane; e < e1; e += 64) {
-                const int c = s_col[e];
-                if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) atomicAdd(&acc[c - c0], s_val[e]);
-              }
+      };
+      // steps [jlo, jhi) overlap the window; their bounds go through VGPRs (readlane) in blocks
+      // of 64 so the only LDS traffic per step is the entries themselves. The adds are LDS
+      // atomics without return: a wave's LDS operations execute in program order, so entry
+      // (j, c) lands after every (j' < j, c) with no wait on the accumulator; inside one step
+      // the columns are distinct.
+      auto apply = [&](int buf, int w0) {
+        const int wn = min(NB, total - w0);
+        const int jlo = first_step(w0);
+        int jhi = jlo, hj = ns;  // first step starting at or after w0 + wn
+        while (jhi < hj) {
+          const int mid = (jhi + hj) >> 1;
+          if (s_pref[mid] < w0 + wn) jhi = mid + 1; else hj = mid;
+        }
+        for (int jb2 = jlo; jb2 < jhi; jb2 += 64) {
+          const int nj = min(64, jhi - jb2);
+          const int p0 = lane < nj ? s_pref[jb2 + lane] : 0;
+          const int p1 = lane < nj ? s_pref[jb2 + lane + 1] : 0;
+          for (int q = 0; q < nj; ++q) {
+            const int e0 = max(__builtin_amdgcn_readlane(p0, q), w0) - w0;
+            const int e1 = min(__builtin_amdgcn_readlane(p1, q), w0 + wn) - w0;
+            for (int e = e0 + lane; e < e1; e += 64) {
+              const int c = s_col[buf][e];
+              if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) atomicAdd(&acc[c - c0], s_val[buf][e]);
             }
           }
         }
+      };
+      const int n_win = (total + NB - 1) / NB;
+      if (n_win > 0) {
+        stage(0, 0, wave, NW);
+        __syncthreads();
+      }
+      for (int wi = 0; wi < n_win; ++wi) {
+        if (wave < OWN) apply(wi & 1, wi * NB);
+        else if (wi + 1 < n_win) stage((wi + 1) & 1, (wi + 1) * NB, wave - OWN, NW - OWN);
         __syncthreads();
       }
     }
@@ -288,7 +304,7 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
     const int32_t* __restrict__ order, const int32_t* __restrict__ a_ptr, const int32_t* __restrict__ a_idx,
     const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr, const int32_t* __restrict__ b_idx,
     const float* __restrict__ b_val, const int64_t* __restrict__ rowoff, int32_t* __restrict__ t_idx,
-    float* __restrict__ t_val, int64_t* __restrict__ kept) {
+    float* __restrict__ t_val, int64_t* __restrict__ kept, int64_t n_rows) {
   constexpr int NT = kSmallNT, NB = kSmallProducts, NW = NT / 64;
   __shared__ uint32_t s_key[NB];
   __shared__ TACC s_val[NB];
@@ -297,7 +313,9 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
   __shared__ TACC s_av[NT];
   __shared__ int32_t s_wsum[NW];
   const int t = threadIdx.x;
-  const int64_t row = order[blockIdx.x];
+  // one row per workgroup by default; a capped grid walks the rows (experiment knob)
+  for (int64_t ri = blockIdx.x; ri < n_rows; ri += gridDim.x) {
+  const int64_t row = order[ri];
   const int32_t a0 = a_ptr[row];
   const int ns = a_ptr[row + 1] - a0;  // <= NT (host-side classification)
   int len = 0;
@@ -371,6 +389,8 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
     }
   }
   if (t == 0) kept[row] = n_kept;
+  __syncthreads();  // LDS reuse by the next row
+  }
 }
 
 // C rows from the upper-bound layout: row i's kept entries at rowoff[i] -> c_ptr[i]. One wave
@@ -466,35 +486,22 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
                                          [](uint32_t a, uint32_t b) { return a > b; }) - skey.begin();
   auto* tidx = static_cast<int32_t*>(b_tidx.p);
   auto* tval = static_cast<float*>(b_tval.p);
-  // The two row sets are independent: the small-row kernel (~20-29 KB of LDS) runs on a side
-  // stream so its workgroups fill the LDS a dense-slab workgroup (131-148 KB) leaves free.
-  hipStream_t side = nullptr;
-  hipEvent_t ev_ready = nullptr, ev_small = nullptr;
-  const bool both = n_big > 0 && m - n_big > 0;
-  if (both) {
-    GCG_HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
-    GCG_HIP_CHECK(hipEventCreateWithFlags(&ev_ready, hipEventDisableTiming));
-    GCG_HIP_CHECK(hipEventCreateWithFlags(&ev_small, hipEventDisableTiming));
-    GCG_HIP_CHECK(hipEventRecord(ev_ready, st));
-    GCG_HIP_CHECK(hipStreamWaitEvent(side, ev_ready, 0));
-  }
-  hipStream_t st_small = both ? side : st;
+  // Measured (tools/exp_spgemm_knobs.py, Twitter-World): the small-row kernel on a side stream
+  // beside the dense-slab kernel ran 5x SLOWER (615 vs 112 ms; the two kernels' workgroups
+  // compete for LDS), and a persistent grid was no faster than one workgroup per row -- so one
+  // stream, one workgroup per row (GCG_SPGEMM_SMALL_GRID caps the grid for experiments).
+  const int small_grid = env_int("GCG_SPGEMM_SMALL_GRID");
   if (m - n_big > 0)
-    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>), dim3(static_cast<unsigned>(m - n_big)), dim3(kSmallNT),
-                       0, st_small, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx, tval,
-                       kept);
+    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>),
+                       dim3(static_cast<unsigned>(small_grid > 0 ? std::min<int64_t>(m - n_big, small_grid)
+                                                                 : m - n_big)),
+                       dim3(kSmallNT), 0, st, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev,
+                       tidx, tval, kept, m - n_big);
   if (n_big > 0)
     hipLaunchKernelGGL((spgemm_rows_kernel<TA, TACC, SMAX>), dim3(static_cast<unsigned>(n_big)), dim3(kRowsNT), 0, st,
                        p, static_cast<int>(sw), id2, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
                        tval, kept);
   const hipError_t launch_err = hipGetLastError();
-  if (both) {
-    (void)hipEventRecord(ev_small, side);
-    (void)hipStreamWaitEvent(st, ev_small, 0);
-    (void)hipEventDestroy(ev_ready);
-    (void)hipEventDestroy(ev_small);
-    (void)hipStreamDestroy(side);  // returns at once; the queued work completes
-  }
   if (launch_err != hipSuccess) return fail(GCG_ERR_HIP, "SpGEMM row kernels: %s", hipGetErrorString(launch_err));
   tb = t_scan;
   GCG_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(b_tmp.p, tb, kept, cp64, static_cast<int>(m + 1), st));
