@@ -204,8 +204,10 @@ gcg_status gcg_normalize_adjacency_f32(int64_t n, int64_t n_edges, const int32_t
  * float64, the reference's H64 * X32 upcast), exact zero sums dropped (as scipy), then
  * rounded to float32. Output CSR is canonical (sorted columns), as astype() leaves it.
  * Step 1: gcg_spgemm_products -> number of products P (synchronizes). Step 2: gcg_spgemm
- * with c_idx/c_val of capacity P, c_ptr of m+1; actual nnz to *nnz_c_dev. Not a hot-path
- * call: it allocates stream-ordered temporaries (~32 B per product) and synchronizes.
+ * with c_idx/c_val of capacity P, c_ptr of m+1; actual nnz to *nnz_c_dev (<= INT32_MAX).
+ * Not a hot-path call: it allocates stream-ordered temporaries (~8 B per product on the
+ * row-wise path, ~40 B per product per 2^29-product row chunk on the expand-sort-reduce
+ * path used when p exceeds 8 LDS slabs) and synchronizes.
  */
 gcg_status gcg_spgemm_products(int64_t m, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
                                int64_t n, const int32_t* b_ptr, int64_t* n_products,
