@@ -15,3 +15,6 @@ grep '^{' $out/train_${cfg}_${order}.log | python3 -c "import json,sys; r=json.l
 done; done
 timeout -k 10 600 python -u bench.py > $out/bench.log 2>&1 || { tail -20 $out/bench.log; exit 1; }
 grep '^{' $out/bench.log | cut -c1-700
+timeout -k 10 600 python -u tools/bench_graph.py > $out/bench_graph.log 2>&1 || { tail -20 $out/bench_graph.log; exit 1; }
+grep '^{' $out/bench_graph.log | cut -c1-400
+bash tools/gpu/prof_spgemm.sh > $out/prof_spgemm.log 2>&1 || { tail -20 $out/prof_spgemm.log; exit 1; }
