@@ -192,19 +192,24 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
     const int64_t c1 = min(p, c0 + sw);
     for (int32_t jb = a0; jb < a1; jb += NT) {
       const int ns = min(NT, a1 - jb);
-      int len = 0;
-      if (t < ns) {
-        const int32_t r = a_idx[jb + t];
-        const int32_t b0 = b_ptr[r];
-        len = b_ptr[r + 1] - b0;
-        s_bst[t] = b0;
-        s_av[t] = static_cast<TACC>(a_val[jb + t]);
+      // step table (B-row starts, A values, prefix of B-row lengths); a row of at most NT
+      // nonzeros keeps it from the first slab
+      if (sl == 0 || a1 - a0 > NT) {
+        int len = 0;
+        if (t < ns) {
+          const int32_t r = a_idx[jb + t];
+          const int32_t b0 = b_ptr[r];
+          len = b_ptr[r + 1] - b0;
+          s_bst[t] = b0;
+          s_av[t] = static_cast<TACC>(a_val[jb + t]);
+        }
+        int tot;
+        const int excl = block_excl_scan<NW>(len, s_wsum, tot);
+        s_pref[t] = excl;
+        if (t == 0) s_pref[NT] = tot;
+        __syncthreads();
       }
-      int total;
-      const int excl = block_excl_scan<NW>(len, s_wsum, total);
-      s_pref[t] = excl;
-      if (t == 0) s_pref[NT] = total;
-      __syncthreads();
+      const int total = s_pref[NT];
       // first step overlapping the window starting at w0: last j with s_pref[j] <= w0
       auto first_step = [&](int w0) {
         int lo = 0, hi = ns - 1;
