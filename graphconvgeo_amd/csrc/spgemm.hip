@@ -295,9 +295,9 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
 
 
 // Rows with at most kSmallSteps nonzeros and kSmallProducts products skip the slabs: the
-// workgroup stages the row's products (key = column << 11 | traversal position), bitonic-sorts
+// workgroup stages the row's products (key = column << 11 | traversal position), radix-sorts
 // the keys in LDS, and sums every run of equal columns in position order -- the same
-// csr_matmat order, independent of the number of output columns. 256 threads, ~21 KB of LDS
+// csr_matmat order, independent of the number of output columns. 256 threads, 20-29 KB of LDS
 // (several workgroups per CU); the bulk of a power-law graph's rows.
 constexpr int kSmallNT = 256;
 constexpr int kSmallSteps = kSmallNT;
@@ -309,9 +309,17 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
     const int32_t* __restrict__ order, const int32_t* __restrict__ a_ptr, const int32_t* __restrict__ a_idx,
     const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr, const int32_t* __restrict__ b_idx,
     const float* __restrict__ b_val, const int64_t* __restrict__ rowoff, int32_t* __restrict__ t_idx,
-    float* __restrict__ t_val, int64_t* __restrict__ kept, int64_t n_rows) {
+    float* __restrict__ t_val, int64_t* __restrict__ kept, int64_t n_rows, int col_bits) {
   constexpr int NT = kSmallNT, NB = kSmallProducts, NW = NT / 64;
-  __shared__ uint32_t s_key[NB];
+  using Sort2 = hipcub::BlockRadixSort<uint32_t, NT, 2>;  // rows of <= 512 products
+  using Sort8 = hipcub::BlockRadixSort<uint32_t, NT, 8>;  // <= 2,048
+  // the keys are sorted in registers, so their LDS image can hold the sort's scratch
+  __shared__ union {
+    uint32_t key[NB];
+    typename Sort2::TempStorage t2;
+    typename Sort8::TempStorage t8;
+  } s_u;
+  uint32_t* s_key = s_u.key;
   __shared__ TACC s_val[NB];
   __shared__ int32_t s_pref[NT + 1];
   __shared__ int32_t s_bst[NT];
@@ -352,21 +360,29 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
     s_key[q] = key;
   }
   __syncthreads();
-  for (int k = 2; k <= sz; k <<= 1) {  // bitonic sort, ascending; keys are unique
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = t; i < sz; i += NT) {
-        const int ixj = i ^ j;
-        if (ixj > i) {
-          const uint32_t x = s_key[i], y = s_key[ixj];
-          if ((x > y) == ((i & k) == 0)) {
-            s_key[i] = y;
-            s_key[ixj] = x;
-          }
-        }
-      }
-      __syncthreads();
-    }
+  // Stable LSD radix sort of the blocked keys on their column bits [11, 11 + col_bits): the
+  // positions (low 11 bits) enter in traversal order, so equal columns stay in csr_matmat
+  // order. Pad keys (all ones) sort last.
+  if (sz <= 2 * NT) {
+    uint32_t k[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) k[i] = t * 2 + i < sz ? s_key[t * 2 + i] : 0xffffffffu;
+    __syncthreads();
+    Sort2(s_u.t2).Sort(k, 11, 11 + col_bits);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i) s_key[t * 2 + i] = k[i];
+  } else {
+    uint32_t k[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) k[i] = t * 8 + i < sz ? s_key[t * 8 + i] : 0xffffffffu;
+    __syncthreads();
+    Sort8(s_u.t8).Sort(k, 11, 11 + col_bits);
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 8; ++i) s_key[t * 8 + i] = k[i];
   }
+  __syncthreads();
   // runs of equal columns: thread t owns sorted positions [t*per, (t+1)*per) and sums the
   // runs that START there, in position order
   const int per = (total + NT - 1) / NT;
@@ -496,12 +512,14 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   // compete for LDS), and a persistent grid was no faster than one workgroup per row -- so one
   // stream, one workgroup per row (GCG_SPGEMM_SMALL_GRID caps the grid for experiments).
   const int small_grid = env_int("GCG_SPGEMM_SMALL_GRID");
+  int col_bits = 1;  // (1 << col_bits) > p: the pad key's column bits exceed every column
+  while ((int64_t{1} << col_bits) <= p) ++col_bits;
   if (m - n_big > 0)
     hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>),
                        dim3(static_cast<unsigned>(small_grid > 0 ? std::min<int64_t>(m - n_big, small_grid)
                                                                  : m - n_big)),
                        dim3(kSmallNT), 0, st, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev,
-                       tidx, tval, kept, m - n_big);
+                       tidx, tval, kept, m - n_big, col_bits);
   if (n_big > 0)
     hipLaunchKernelGGL((spgemm_rows_kernel<TA, TACC, SMAX>), dim3(static_cast<unsigned>(n_big)), dim3(kRowsNT), 0, st,
                        p, static_cast<int>(sw), id2, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
