@@ -434,6 +434,54 @@ __global__ void spgemm_compact_kernel(int64_t m, const int64_t* __restrict__ row
   }
 }
 
+// In-place form: rows [r0, r1) move left inside the caller's capacity-P output, from the
+// upper-bound layout (rowoff) to the compact one (cptr64 <= rowoff). The host schedules the
+// row ranges so every destination of a launch lies before every source it reads
+// (cptr64[r1] <= rowoff[r0]); a single row may overlap itself, which a wave's forward copy
+// handles (each iteration's loads complete before its stores, and d <= s). No __restrict__:
+// source and destination are the same arrays.
+__global__ void spgemm_compact_inplace_kernel(int64_t r0, int64_t r1, const int64_t* __restrict__ rowoff,
+                                              const int64_t* __restrict__ cptr64, int32_t* idx, float* val) {
+  const int lane = threadIdx.x & 63;
+  const int64_t waves = static_cast<int64_t>(gridDim.x) * (blockDim.x / 64);
+  for (int64_t r = r0 + static_cast<int64_t>(blockIdx.x) * (blockDim.x / 64) + (threadIdx.x >> 6); r < r1;
+       r += waves) {
+    const int64_t d = cptr64[r], s = rowoff[r], n = cptr64[r + 1] - d;
+    if (d == s) continue;
+    for (int64_t k = lane; k < n; k += 64) {
+      const int32_t i = idx[s + k];
+      const float v = val[s + k];
+      idx[d + k] = i;
+      val[d + k] = v;
+    }
+  }
+}
+
+__global__ void cptr32_kernel(int64_t m, const int64_t* __restrict__ cptr64, int32_t* __restrict__ c_ptr) {
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i <= m; i += stride)
+    c_ptr[i] = static_cast<int32_t>(cptr64[i]);
+}
+
+// Row ranges for the in-place compaction: rows already in place (cptr == rowoff) are skipped;
+// a range starting at r0 extends while its destinations end at or before rowoff[r0]. The gap
+// rowoff - cptr only grows with the row, so ranges get longer as rows merge products.
+std::vector<std::pair<int64_t, int64_t>> inplace_ranges(const std::vector<int64_t>& rowoff,
+                                                        const std::vector<int64_t>& cptr) {
+  std::vector<std::pair<int64_t, int64_t>> out;
+  const int64_t m = static_cast<int64_t>(rowoff.size()) - 1;
+  int64_t r0 = 0;
+  while (r0 < m && cptr[r0] == rowoff[r0]) ++r0;
+  while (r0 < m) {
+    int64_t r1 = r0 + 1;
+    while (r1 < m && cptr[r1 + 1] <= rowoff[r0]) ++r1;
+    out.emplace_back(r0, r1);
+    r0 = r1;
+  }
+  return out;
+}
+constexpr size_t kMaxInplaceLaunches = 256;
+
 // Row products (clamped to int32) for the longest-first order.
 // Rows that the small-row kernel cannot take (more than kSmallSteps nonzeros) are keyed
 // above kSmallProducts so they sort into the dense-slab set.
@@ -457,14 +505,17 @@ constexpr int kRowsMaxSlabs = 8;
 template <typename TA, typename TACC>
 gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
                        const TA* a_val, const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
-                       int64_t n_products, const int64_t* rowoff_dev, int32_t* c_ptr, int32_t* c_idx,
-                       float* c_val, int64_t* nnz_c_dev, hipStream_t st) {
-  (void)nnz_a;
+                       int64_t n_products, const int64_t* rowoff_dev, const std::vector<int64_t>& rowoff,
+                       int32_t* c_ptr, int32_t* c_idx, float* c_val, int64_t* nnz_c_dev, hipStream_t st) {
+  (void)nnz_a; (void)n_products;
   constexpr int SMAX = RowsSlab<TACC>::kMax;
   const int64_t n_slabs = (p + SMAX - 1) / SMAX;
   int64_t sw = (p + n_slabs - 1) / n_slabs;
   sw = std::max<int64_t>(kRowsNT, (sw + kRowsNT - 1) / kRowsNT * kRowsNT);
-  DevBuf b_key, b_key2, b_id, b_id2, b_tidx, b_tval, b_kept, b_cp64, b_tmp;
+  // The row kernels write C in the upper-bound layout (row i at rowoff[i]) straight into the
+  // caller's capacity-P c_idx / c_val, which are then compacted in place: no products-sized
+  // temporary (21 GB at Twitter-World) is allocated per call.
+  DevBuf b_key, b_key2, b_id, b_id2, b_kept, b_cp64, b_tmp;
   size_t t_sort = 0, t_scan = 0;
   {
     uint32_t* k = nullptr; int32_t* v = nullptr; int64_t* o = nullptr;
@@ -480,8 +531,6 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   if (e == hipSuccess) e = alloc(b_key2, m * sizeof(uint32_t));
   if (e == hipSuccess) e = alloc(b_id, m * sizeof(int32_t));
   if (e == hipSuccess) e = alloc(b_id2, m * sizeof(int32_t));
-  if (e == hipSuccess) e = alloc(b_tidx, n_products * sizeof(int32_t));
-  if (e == hipSuccess) e = alloc(b_tval, n_products * sizeof(float));
   if (e == hipSuccess) e = alloc(b_kept, (m + 1) * sizeof(int64_t));
   if (e == hipSuccess) e = alloc(b_cp64, (m + 1) * sizeof(int64_t));
   if (e == hipSuccess) e = alloc(b_tmp, std::max(t_sort, t_scan));
@@ -505,8 +554,8 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   GCG_HIP_CHECK(hipStreamSynchronize(st));
   const int64_t n_big = std::lower_bound(skey.begin(), skey.end(), static_cast<uint32_t>(kSmallProducts),
                                          [](uint32_t a, uint32_t b) { return a > b; }) - skey.begin();
-  auto* tidx = static_cast<int32_t*>(b_tidx.p);
-  auto* tval = static_cast<float*>(b_tval.p);
+  auto* tidx = c_idx;
+  auto* tval = c_val;
   // Measured (tools/exp_spgemm_knobs.py, Twitter-World): the small-row kernel on a side stream
   // beside the dense-slab kernel ran 5x SLOWER (615 vs 112 ms; the two kernels' workgroups
   // compete for LDS), and a persistent grid was no faster than one workgroup per row -- so one
@@ -528,12 +577,28 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   if (launch_err != hipSuccess) return fail(GCG_ERR_HIP, "SpGEMM row kernels: %s", hipGetErrorString(launch_err));
   tb = t_scan;
   GCG_HIP_CHECK(hipcub::DeviceScan::ExclusiveSum(b_tmp.p, tb, kept, cp64, static_cast<int>(m + 1), st));
-  int64_t nnz_c = 0;
-  GCG_HIP_CHECK(hipMemcpyAsync(&nnz_c, cp64 + m, sizeof(int64_t), hipMemcpyDeviceToHost, st));
+  std::vector<int64_t> cptr(m + 1);
+  GCG_HIP_CHECK(hipMemcpyAsync(cptr.data(), cp64, (m + 1) * sizeof(int64_t), hipMemcpyDeviceToHost, st));
   GCG_HIP_CHECK(hipStreamSynchronize(st));
+  const int64_t nnz_c = cptr[m];
   if (nnz_c > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "nnz(C) = %lld exceeds int32 CSR", (long long)nnz_c);
-  hipLaunchKernelGGL(spgemm_compact_kernel, dim3(grid_for(m * 64)), dim3(256), 0, st, m, rowoff_dev, cp64,
-                     static_cast<const int32_t*>(b_tidx.p), static_cast<const float*>(b_tval.p), c_ptr, c_idx, c_val);
+  hipLaunchKernelGGL(cptr32_kernel, dim3(grid_for(m + 1)), dim3(256), 0, st, m, cp64, c_ptr);
+  const auto ranges = inplace_ranges(rowoff, cptr);
+  if (ranges.size() <= kMaxInplaceLaunches && env_int("GCG_SPGEMM_COMPACT_TMP") == 0) {
+    for (const auto& rg : ranges)
+      hipLaunchKernelGGL(spgemm_compact_inplace_kernel, dim3(grid_for((rg.second - rg.first) * 64)), dim3(256), 0,
+                         st, rg.first, rg.second, rowoff_dev, cp64, c_idx, c_val);
+  } else {  // rows that merge few products: compact through an nnz(C)-sized temporary instead
+    DevBuf b_cidx, b_cval;
+    e = alloc(b_cidx, nnz_c * sizeof(int32_t));
+    if (e == hipSuccess) e = alloc(b_cval, nnz_c * sizeof(float));
+    if (e != hipSuccess) return fail(GCG_ERR_ALLOC, "SpGEMM compaction temporary: %s", hipGetErrorString(e));
+    hipLaunchKernelGGL(spgemm_compact_kernel, dim3(grid_for(m * 64)), dim3(256), 0, st, m, rowoff_dev, cp64,
+                       c_idx, c_val, c_ptr, static_cast<int32_t*>(b_cidx.p), static_cast<float*>(b_cval.p));
+    GCG_HIP_CHECK(hipGetLastError());
+    GCG_HIP_CHECK(hipMemcpyAsync(c_idx, b_cidx.p, nnz_c * sizeof(int32_t), hipMemcpyDeviceToDevice, st));
+    GCG_HIP_CHECK(hipMemcpyAsync(c_val, b_cval.p, nnz_c * sizeof(float), hipMemcpyDeviceToDevice, st));
+  }
   GCG_HIP_CHECK(hipGetLastError());
   GCG_HIP_CHECK(hipMemcpyAsync(nnz_c_dev, cp64 + m, sizeof(int64_t), hipMemcpyDeviceToDevice, st));
   GCG_HIP_CHECK(hipStreamSynchronize(st));  // temporaries are freed stream-ordered on return
@@ -600,7 +665,7 @@ gcg_status spgemm_impl(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int
   if (m <= INT32_MAX && (p + RowsSlab<TACC>::kMax - 1) / RowsSlab<TACC>::kMax <= kRowsMaxSlabs &&
       env_int("GCG_SPGEMM_ESC") == 0)
     return spgemm_rows<TA, TACC>(m, p, nnz_a, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, n_products, rowoff_dev,
-                                 c_ptr, c_idx, c_val, nnz_c_dev, st);
+                                 rowoff, c_ptr, c_idx, c_val, nnz_c_dev, st);
   const int64_t kChunkProducts = chunk_products();
   std::vector<int64_t> cuts{0};  // greedy row chunks of <= kChunkProducts products (>= 1 row)
   while (cuts.back() < m) {

@@ -575,4 +575,7 @@ def spgemm(A: DeviceCSR, B: DeviceCSR, accumulate_f64: bool = False,
              _ptr(a_vals), is64, B.nnz, _ptr(B.indptr), _ptr(B.indices), _ptr(B.data), acc64,
              P.value, _ptr(c_ptr), _ptr(c_idx), _ptr(c_val), _ptr(nnz), stream)
     m = int(nnz.item())
-    return DeviceCSR(c_ptr, c_idx[:m], c_val[:m], (A.n_rows, B.n_cols), validate=False)
+    # exact-size copies: the capacity-P buffers (products; 2.5x nnz(C) at Twitter-World) go
+    # back to the caching allocator and serve the next call instead of staying pinned by C
+    with torch.cuda.device(dev):
+        return DeviceCSR(c_ptr, c_idx[:m].clone(), c_val[:m].clone(), (A.n_rows, B.n_cols), validate=False)

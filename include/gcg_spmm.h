@@ -205,9 +205,11 @@ gcg_status gcg_normalize_adjacency_f32(int64_t n, int64_t n_edges, const int32_t
  * rounded to float32. Output CSR is canonical (sorted columns), as astype() leaves it.
  * Step 1: gcg_spgemm_products -> number of products P (synchronizes). Step 2: gcg_spgemm
  * with c_idx/c_val of capacity P, c_ptr of m+1; actual nnz to *nnz_c_dev (<= INT32_MAX).
- * Not a hot-path call: it allocates stream-ordered temporaries (~8 B per product on the
- * row-wise path, ~40 B per product per 2^29-product row chunk on the expand-sort-reduce
- * path used when p exceeds 8 LDS slabs) and synchronizes.
+ * Not a hot-path call: it allocates stream-ordered temporaries and synchronizes. The
+ * row-wise path (p within 8 LDS slabs) uses c_idx/c_val themselves as its products-sized
+ * scratch (C rows written at their product offsets, then compacted in place), so it only
+ * allocates ~30 B per row of A; the expand-sort-reduce path used for wider p allocates ~40 B
+ * per product per 2^29-product row chunk. Entries of c_idx/c_val past nnz(C) are undefined.
  */
 gcg_status gcg_spgemm_products(int64_t m, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
                                int64_t n, const int32_t* b_ptr, int64_t* n_products,

@@ -140,7 +140,7 @@ def test_project_xent_autograd_vs_float64(cuda):
     logits64 = P.astype(np.float64) @ W + b
     _, loss64, hits64, G64 = O.softmax_xent_f64(logits64, y)
     G64 = G64 * 2.5
-    assert abs(float(loss) - loss64.mean()) < 1e-5
+    assert abs(float(loss.detach()) - loss64.mean()) < 1e-5
     assert np.abs(Pt.grad.cpu().numpy() - G64 @ W.T.astype(np.float64)).max() < 1e-6
     assert np.abs(Wt.grad.cpu().numpy() - P.T.astype(np.float64) @ G64).max() < 1e-5
     assert np.abs(bt.grad.cpu().numpy() - G64.sum(0)).max() < 1e-5

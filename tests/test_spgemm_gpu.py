@@ -160,3 +160,30 @@ def test_spgemm_rows_kernel_shapes(cuda, monkeypatch, path, p):
     Cacc = gs.spgemm(Ad, Bd, accumulate_f64=True).to_scipy()  # f32 A, float64 sums
     refacc = canon((A.astype(np.float64) @ B.astype(np.float64)).astype(np.float32))
     assert np.array_equal(Cacc.indices, refacc.indices) and np.array_equal(Cacc.data, refacc.data)
+
+
+@pytest.mark.parametrize("compact", ["inplace", "tmp"])
+def test_spgemm_compaction_forms(cuda, monkeypatch, compact):
+    """C rows are computed at their product offsets inside c_idx/c_val and compacted there (row
+    ranges whose destinations precede their sources), or through an nnz(C) temporary when that
+    would take too many launches. Rows that merge nothing (in place), rows that merge a little
+    (short ranges, single rows overlapping themselves) and rows that merge a lot, mixed."""
+    monkeypatch.setenv("GCG_SPGEMM_COMPACT_TMP", "1" if compact == "tmp" else "0")
+    rng = np.random.default_rng(11)
+    n, p = 3000, 5000
+    # rows of A: first 500 rows one step each (no merging: in place), then rows of 2 steps
+    # sharing a few columns (small gaps), then dense rows sharing many columns
+    rows, cols = [], []
+    for i in range(n):
+        k = 1 if i < 500 else (2 if i < 2000 else 40)
+        rows += [i] * k
+        cols += list(rng.choice(n, k, replace=False))
+    A = sps.csr_matrix((rng.standard_normal(len(rows)).astype(np.float32), (rows, cols)), shape=(n, n))
+    B = sps.random(n, p, density=0.01, random_state=6, format="csr", dtype=np.float32)
+    B.data = rng.standard_normal(B.nnz).astype(np.float32)
+    C = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
+    ref = canon(A @ B)
+    assert ref.nnz < int(np.diff(B.indptr)[A.indices].sum())  # some rows merged
+    assert np.array_equal(C.indptr, ref.indptr)
+    assert np.array_equal(C.indices, ref.indices)
+    assert np.array_equal(C.data, ref.data)
