@@ -129,7 +129,8 @@ struct DevBuf {
 // One 1024-thread workgroup per row of C, rows dispatched longest-first. The row's products
 // are staged through LDS in traversal order (A row storage order, then B row order), NB at a
 // time, and added into a dense LDS accumulator that covers a slab of `sw` output columns.
-// OWN = 4 owner waves apply them: wave w adds exactly the columns c with c % 4 == w and walks
+// OWN = 2 owner waves apply them (measured: 4 -> 2 owners 55.1 -> 53.8 ms at Twitter-World; 1
+// owner 52.9 but Twitter-US 7.2 -> 7.6): wave w adds exactly the columns c with c % OWN == w and walks
 // the steps (nonzeros of the A row) in order, so every C entry receives its products in
 // scipy csr_matmat's order (sums[k] += v * Bx[kk], from 0) without atomics; inside one step
 // the columns are distinct (a CSR row), so the lanes of a wave never collide. Extraction
@@ -170,7 +171,7 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
     int32_t* __restrict__ t_idx, float* __restrict__ t_val, int64_t* __restrict__ kept) {
   // NB products per staging buffer, two buffers: waves OWN.. stage window w+1 while the
   // owner waves apply window w
-  constexpr int NT = kRowsNT, NB = sizeof(TACC) == 8 ? kRowsNB / 2 : kRowsNB, NW = NT / 64, OWN = 4;
+  constexpr int NT = kRowsNT, NB = sizeof(TACC) == 8 ? kRowsNB / 2 : kRowsNB, NW = NT / 64, OWN = 2;
   __shared__ TACC acc[SMAX];
   __shared__ int32_t s_col[2][NB];
   __shared__ TACC s_val[2][NB];
@@ -221,15 +222,44 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
       };
       // stage positions [w0, w0 + wn) into buffer `buf`: stager wave v of nv copies steps
       // jlo + v, jlo + v + nv, ... (one coalesced B-row read per step)
+      // SU steps per round: their first 64 positions are loaded before any is stored, so a
+      // stager wave keeps SU B-row reads in flight instead of one; positions past the first 64
+      // of a step (B rows longer than a wave) follow in a remainder loop.
       auto stage = [&](int buf, int w0, int v, int nv) {
-        const int wn = min(NB, total - w0);
-        for (int j = first_step(w0) + v; j < ns && s_pref[j] < w0 + wn; j += nv) {
-          const int e0 = max(s_pref[j], w0), e1 = min(s_pref[j + 1], w0 + wn);
-          const int32_t kb = s_bst[j] - s_pref[j];
-          const TACC av = s_av[j];
-          for (int pos = e0 + lane; pos < e1; pos += 64) {
-            s_col[buf][pos - w0] = b_idx[kb + pos];
-            s_val[buf][pos - w0] = av * static_cast<TACC>(b_val[kb + pos]);
+        constexpr int SU = 4;
+        const int wn = min(NB, total - w0), wend = w0 + wn;
+        for (int j = first_step(w0) + v; j < ns && s_pref[j] < wend; j += SU * nv) {
+          int32_t ci[SU];
+          float bv[SU];
+          int e0[SU], e1[SU], kb[SU];
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int jj = j + u * nv;
+            const bool ok = jj < ns && s_pref[jj] < wend;
+            e0[u] = ok ? max(s_pref[jj], w0) : 0;
+            e1[u] = ok ? min(s_pref[jj + 1], wend) : 0;
+            kb[u] = ok ? s_bst[jj] - s_pref[jj] : 0;
+            const int pos = e0[u] + lane;
+            if (pos < e1[u]) {
+              ci[u] = b_idx[kb[u] + pos];
+              bv[u] = b_val[kb[u] + pos];
+            }
+          }
+#pragma unroll
+          for (int u = 0; u < SU; ++u) {
+            const int pos = e0[u] + lane;
+            if (pos < e1[u]) {
+              const TACC av = s_av[j + u * nv];
+              s_col[buf][pos - w0] = ci[u];
+              s_val[buf][pos - w0] = av * static_cast<TACC>(bv[u]);
+            }
+            if (e1[u] - e0[u] > 64) {
+              const TACC av = s_av[j + u * nv];
+              for (int q = e0[u] + 64 + lane; q < e1[u]; q += 64) {
+                s_col[buf][q - w0] = b_idx[kb[u] + q];
+                s_val[buf][q - w0] = av * static_cast<TACC>(b_val[kb[u] + q]);
+              }
+            }
           }
         }
       };
@@ -246,16 +276,35 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
           const int mid = (jhi + hj) >> 1;
           if (s_pref[mid] < w0 + wn) jhi = mid + 1; else hj = mid;
         }
+        // AU steps per round: their first 64 entries are read from LDS before any add is
+        // issued (AU reads in flight), then added in step order; entries past the first 64
+        // of a step follow in order before the next step's.
+        constexpr int AU = 8;
         for (int jb2 = jlo; jb2 < jhi; jb2 += 64) {
           const int nj = min(64, jhi - jb2);
           const int p0 = lane < nj ? s_pref[jb2 + lane] : 0;
           const int p1 = lane < nj ? s_pref[jb2 + lane + 1] : 0;
-          for (int q = 0; q < nj; ++q) {
-            const int e0 = max(__builtin_amdgcn_readlane(p0, q), w0) - w0;
-            const int e1 = min(__builtin_amdgcn_readlane(p1, q), w0 + wn) - w0;
-            for (int e = e0 + lane; e < e1; e += 64) {
-              const int c = s_col[buf][e];
-              if ((c & (OWN - 1)) == wave && c >= c0 && c < c1) atomicAdd(&acc[c - c0], s_val[buf][e]);
+          for (int q = 0; q < nj; q += AU) {
+            int cc[AU], e0[AU], e1[AU];
+            TACC vv[AU];
+#pragma unroll
+            for (int u = 0; u < AU; ++u) {
+              const int qq = min(q + u, 63);
+              const bool ok = q + u < nj;
+              e0[u] = ok ? max(__builtin_amdgcn_readlane(p0, qq), w0) - w0 : 0;
+              e1[u] = ok ? min(__builtin_amdgcn_readlane(p1, qq), w0 + wn) - w0 : 0;
+              const int e = e0[u] + lane;
+              cc[u] = e < e1[u] ? s_col[buf][e] : -1;
+              vv[u] = e < e1[u] ? s_val[buf][e] : TACC(0);
+            }
+#pragma unroll
+            for (int u = 0; u < AU; ++u) {
+              const int c = cc[u];
+              if (c >= 0 && (c & (OWN - 1)) == wave && c >= c0 && c < c1) atomicAdd(&acc[c - c0], vv[u]);
+              for (int e = e0[u] + 64 + lane; e < e1[u]; e += 64) {
+                const int c2 = s_col[buf][e];
+                if ((c2 & (OWN - 1)) == wave && c2 >= c0 && c2 < c1) atomicAdd(&acc[c2 - c0], s_val[buf][e]);
+              }
             }
           }
         }
@@ -310,9 +359,9 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
     const TA* __restrict__ a_val, const int32_t* __restrict__ b_ptr, const int32_t* __restrict__ b_idx,
     const float* __restrict__ b_val, const int64_t* __restrict__ rowoff, int32_t* __restrict__ t_idx,
     float* __restrict__ t_val, int64_t* __restrict__ kept, int64_t n_rows, int col_bits) {
-  constexpr int NT = kSmallNT, NB = kSmallProducts, NW = NT / 64;
-  using Sort2 = hipcub::BlockRadixSort<uint32_t, NT, 2>;  // rows of <= 512 products
-  using Sort8 = hipcub::BlockRadixSort<uint32_t, NT, 8>;  // <= 2,048
+  constexpr int NT = kSmallNT, NB = kSmallProducts, NW = NT / 64, KPT8 = 8;
+  using Sort2 = hipcub::BlockRadixSort<uint32_t, NT, 2>;     // rows of <= 512 products
+  using Sort8 = hipcub::BlockRadixSort<uint32_t, NT, KPT8>;  // <= 2,048
   // the keys are sorted in registers, so their LDS image can hold the sort's scratch
   __shared__ union {
     uint32_t key[NB];
@@ -373,14 +422,14 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
 #pragma unroll
     for (int i = 0; i < 2; ++i) s_key[t * 2 + i] = k[i];
   } else {
-    uint32_t k[8];
+    uint32_t k[KPT8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) k[i] = t * 8 + i < sz ? s_key[t * 8 + i] : 0xffffffffu;
+    for (int i = 0; i < KPT8; ++i) k[i] = t * KPT8 + i < sz ? s_key[t * KPT8 + i] : 0xffffffffu;
     __syncthreads();
     Sort8(s_u.t8).Sort(k, 11, 11 + col_bits);
     __syncthreads();
 #pragma unroll
-    for (int i = 0; i < 8; ++i) s_key[t * 8 + i] = k[i];
+    for (int i = 0; i < KPT8; ++i) s_key[t * KPT8 + i] = k[i];
   }
   __syncthreads();
   // runs of equal columns: thread t owns sorted positions [t*per, (t+1)*per) and sums the
@@ -563,12 +612,15 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   const int small_grid = env_int("GCG_SPGEMM_SMALL_GRID");
   int col_bits = 1;  // (1 << col_bits) > p: the pad key's column bits exceed every column
   while ((int64_t{1} << col_bits) <= p) ++col_bits;
-  if (m - n_big > 0)
-    hipLaunchKernelGGL((spgemm_small_rows_kernel<TA, TACC>),
-                       dim3(static_cast<unsigned>(small_grid > 0 ? std::min<int64_t>(m - n_big, small_grid)
-                                                                 : m - n_big)),
-                       dim3(kSmallNT), 0, st, id2 + n_big, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev,
-                       tidx, tval, kept, m - n_big, col_bits);
+  auto small_launch = [&](auto kern, int64_t r0, int64_t r1) {
+    if (r1 <= r0) return;
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(small_grid > 0 ? std::min<int64_t>(r1 - r0, small_grid) : r1 - r0)),
+                       dim3(kSmallNT), 0, st, id2 + r0, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
+                       tval, kept, r1 - r0, col_bits);
+  };
+  // measured: a second instance for rows of <= 512 products with a quarter of the LDS (8
+  // workgroups per CU instead of ~5) left the small-row time unchanged (16.2 vs 16.3 ms, World)
+  small_launch(spgemm_small_rows_kernel<TA, TACC>, n_big, m);
   if (n_big > 0)
     hipLaunchKernelGGL((spgemm_rows_kernel<TA, TACC, SMAX>), dim3(static_cast<unsigned>(n_big)), dim3(kRowsNT), 0, st,
                        p, static_cast<int>(sw), id2, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
