@@ -497,11 +497,28 @@ __global__ void spgemm_compact_inplace_kernel(int64_t r0, int64_t r1, const int6
        r += waves) {
     const int64_t d = cptr64[r], s = rowoff[r], n = cptr64[r + 1] - d;
     if (d == s) continue;
-    for (int64_t k = lane; k < n; k += 64) {
-      const int32_t i = idx[s + k];
-      const float v = val[s + k];
-      idx[d + k] = i;
-      val[d + k] = v;
+    // 4 x 64 entries per round: all loads of a round before its stores (d <= s, so a round's
+    // stores never reach a source entry of this or a later round)
+    constexpr int R = 4;
+    for (int64_t k0 = 0; k0 < n; k0 += R * 64) {
+      int32_t iv[R];
+      float vv[R];
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int64_t k = k0 + u * 64 + lane;
+        if (k < n) {
+          iv[u] = idx[s + k];
+          vv[u] = val[s + k];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int64_t k = k0 + u * 64 + lane;
+        if (k < n) {
+          idx[d + k] = iv[u];
+          val[d + k] = vv[u];
+        }
+      }
     }
   }
 }
