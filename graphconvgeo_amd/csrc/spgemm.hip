@@ -211,15 +211,26 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
         __syncthreads();
       }
       const int total = s_pref[NT];
-      // first step overlapping the window starting at w0: last j with s_pref[j] <= w0
-      auto first_step = [&](int w0) {
-        int lo = 0, hi = ns - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (s_pref[mid] <= w0) lo = mid; else hi = mid - 1;
+      // Step lookups are wave-parallel scans from a per-wave hint (windows only move forward):
+      // 64 prefix entries per LDS read + ballot instead of a ~10-read dependent binary search.
+      // first step overlapping the window starting at w0: last j in [from, ns) with
+      // s_pref[j] <= w0 (s_pref[from] <= w0 holds for a hint from an earlier window)
+      auto first_step = [&](int from, int w0) {
+        for (int j0 = from;; j0 += 64) {
+          const int j = j0 + lane;
+          const uint64_t b = __ballot(j >= ns || s_pref[min(j, NT)] > w0);
+          if (b) return j0 + static_cast<int>(__builtin_ctzll(b)) - 1;
         }
-        return lo;
       };
+      // first j in [from, ns] with j == ns or s_pref[j] >= target
+      auto first_ge = [&](int from, int target) {
+        for (int j0 = from;; j0 += 64) {
+          const int j = j0 + lane;
+          const uint64_t b = __ballot(j >= ns || s_pref[min(j, NT)] >= target);
+          if (b) return min(j0 + static_cast<int>(__builtin_ctzll(b)), ns);
+        }
+      };
+      int hint = 0;  // this wave's last window start step (owner and stager waves apart)
       // stage positions [w0, w0 + wn) into buffer `buf`: stager wave v of nv copies steps
       // jlo + v, jlo + v + nv, ... (one coalesced B-row read per step)
       // SU steps per round: their first 64 positions are loaded before any is stored, so a
@@ -228,7 +239,8 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
       auto stage = [&](int buf, int w0, int v, int nv) {
         constexpr int SU = 4;
         const int wn = min(NB, total - w0), wend = w0 + wn;
-        for (int j = first_step(w0) + v; j < ns && s_pref[j] < wend; j += SU * nv) {
+        hint = first_step(hint, w0);
+        for (int j = hint + v; j < ns && s_pref[j] < wend; j += SU * nv) {
           int32_t ci[SU];
           float bv[SU];
           int e0[SU], e1[SU], kb[SU];
@@ -270,12 +282,8 @@ __global__ __launch_bounds__(kRowsNT) void spgemm_rows_kernel(
       // the columns are distinct.
       auto apply = [&](int buf, int w0) {
         const int wn = min(NB, total - w0);
-        const int jlo = first_step(w0);
-        int jhi = jlo, hj = ns;  // first step starting at or after w0 + wn
-        while (jhi < hj) {
-          const int mid = (jhi + hj) >> 1;
-          if (s_pref[mid] < w0 + wn) jhi = mid + 1; else hj = mid;
-        }
+        const int jlo = hint = first_step(hint, w0);
+        const int jhi = first_ge(jlo, w0 + wn);  // first step starting at or after w0 + wn
         // AU steps per round: their first 64 entries are read from LDS before any add is
         // issued (AU reads in flight), then added in step order; entries past the first 64
         // of a step follow in order before the next step's.
