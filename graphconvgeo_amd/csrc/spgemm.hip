@@ -402,6 +402,8 @@ __global__ __launch_bounds__(kSmallNT) void spgemm_small_rows_kernel(
   int sz = 64;
   while (sz < total) sz <<= 1;
   __syncthreads();
+  // one position per thread (binary search for its step); measured faster than staging by
+  // step with 4 B-row reads in flight per wave (World 16.2 vs 17.4 ms)
   for (int q = t; q < sz; q += NT) {
     uint32_t key = 0xffffffffu;
     if (q < total) {
