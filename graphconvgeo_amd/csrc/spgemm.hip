@@ -132,8 +132,9 @@ struct DevBuf {
 // OWN = 2 owner waves apply them (measured: 4 -> 2 owners 55.1 -> 53.8 ms at Twitter-World; 1
 // owner 52.9 but Twitter-US 7.2 -> 7.6): wave w adds exactly the columns c with c % OWN == w and walks
 // the steps (nonzeros of the A row) in order, so every C entry receives its products in
-// scipy csr_matmat's order (sums[k] += v * Bx[kk], from 0) without atomics; inside one step
-// the columns are distinct (a CSR row), so the lanes of a wave never collide. Extraction
+// scipy csr_matmat's order (sums[k] += v * Bx[kk], from 0) through no-return LDS adds that
+// need no ordering beyond the wave's own program order; inside one step the columns are
+// distinct (a CSR row), so the lanes of a wave never collide. Extraction
 // walks the slab in column order (canonical output), keeps sums != 0 (scipy's
 // `if (sums[head] != 0)`) and re-zeroes the slab. Output goes to an upper-bound layout
 // (row i at rowoff[i], its product count prefix) and is compacted afterwards.
