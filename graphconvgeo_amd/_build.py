@@ -33,6 +33,20 @@ def _hipcc() -> str:
     raise RuntimeError("hipcc not found: the graphconvgeo_amd native library cannot be built")
 
 
+def source_hash() -> str:
+    """Content hash of every file the library is built from (sources, headers, flags). Baked
+    into the library (gcg_source_hash) so a stale binary is detected by content, not mtime
+    (a snapshot copied to another machine does not keep mtimes reliably)."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for p in (*SOURCES, *INTERNAL_HEADERS, HEADER):
+        with open(p, "rb") as f:
+            h.update(os.path.basename(p).encode() + b"\0" + f.read() + b"\0")
+    h.update(" ".join(HIPCC_FLAGS).encode())
+    return h.hexdigest()[:16]
+
+
 def needs_build() -> bool:
     if not os.path.exists(LIB):
         return True
@@ -48,12 +62,13 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
     import tempfile
 
     hipcc = _hipcc()
+    digest = source_hash()
     with tempfile.TemporaryDirectory(prefix="gcg_build_") as tmpd:
         objs = [os.path.join(tmpd, os.path.basename(src) + ".o") for src in SOURCES]
 
         def compile_one(src_obj):
             src, obj = src_obj
-            cmd = [hipcc, *HIPCC_FLAGS, "-c", "-o", obj, src]
+            cmd = [hipcc, *HIPCC_FLAGS, f'-DGCG_SOURCE_HASH="{digest}"', "-c", "-o", obj, src]
             if src.endswith(".cpp"):
                 cmd = [hipcc, "-x", "hip", *cmd[1:]]
             if verbose:

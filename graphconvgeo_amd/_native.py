@@ -10,6 +10,7 @@ import ctypes as C
 import os
 import threading
 
+from . import _build
 from ._build import LIB
 
 GCG_OK = 0
@@ -29,6 +30,7 @@ _psz = C.POINTER(C.c_size_t)
 # name -> (restype, argtypes); mirrors include/gcg_spmm.h one to one.
 SIGNATURES = {
     "gcg_version": (C.c_char_p, []),
+    "gcg_source_hash": (C.c_char_p, []),
     "gcg_last_error": (C.c_char_p, []),
     "gcg_spmm_csr_f32": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
                                    C.c_int, _p, _i64, _p]),
@@ -39,6 +41,12 @@ SIGNATURES = {
     "gcg_spmm_plan_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
     "gcg_spmm_csr_f32_planned": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
                                            C.c_int, _p, C.c_size_t, _p]),
+    "gcg_spmm_csr_f32_gate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _i64, _i64, _p, _i64,
+                                        _p, C.c_int, _p, _i64, _p, _i64, _p]),
+    "gcg_spmm_csr_f32_planned_gate": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
+                                                C.c_int, _p, _i64, _p, C.c_size_t, _p]),
+    "gcg_relu_backward_gate_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p,
+                                             C.c_size_t, _p]),
     "gcg_spmm_plan_host": (C.c_int, [_i64, _p, _p, _i64, _i64, C.c_int, _p, _i64, _pi64, _p,
                                      _i64, _pi64, _pi64]),
     "gcg_csr_validate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p]),
@@ -100,8 +108,26 @@ def load() -> C.CDLL:
                 fn = getattr(lib, name)
                 fn.restype = res
                 fn.argtypes = args
+            _check_fresh(lib, path)
             _lib = lib
     return _lib
+
+
+def _check_fresh(lib, path: str) -> None:
+    """Refuse a library built from other sources than the tree's (a stale binary would make
+    every test and bench measure old kernels). GCG_LIB (an explicit library) or
+    GCG_ALLOW_STALE=1 skip the check."""
+    if "GCG_LIB" in os.environ or os.environ.get("GCG_ALLOW_STALE") == "1":
+        return
+    try:
+        want = _build.source_hash()
+    except OSError:  # sources not shipped next to the library: nothing to compare
+        return
+    got = lib.gcg_source_hash().decode()
+    if got != want:
+        raise ImportError(
+            f"{path} was built from other sources (hash {got}, tree {want}); rebuild with "
+            "`python -m graphconvgeo_amd._build` (or __graft_entry__.build())")
 
 
 def call(name: str, *args) -> None:

@@ -106,11 +106,18 @@ int64_t relu_rows_per_block(int64_t M) {
   return std::max<int64_t>(kReluMinRows, (r + 3) / 4 * 4);
 }
 
-template <int VEC, bool MASK>
+// GATE: the mask comes from the gate bytes of the SpMM epilogue (2 / 1 / 0 -> g, g/2, 0:
+// Theano's 0.5*(1 + sgn(x)) rectify gradient) instead of Y > 0.
+__device__ __forceinline__ float gate_apply(float g, uint32_t code) {
+  return code == 2u ? g : (code == 1u ? 0.5f * g : 0.0f);
+}
+
+template <int VEC, bool MASK, bool GATE = false>
 __global__ __launch_bounds__(256) void relu_backward_kernel(
     int64_t M, int K, int64_t rows_per_block, const float* gY, int64_t ldg,
     const float* __restrict__ Y, int64_t ldy, float* g_out, int64_t ldo,
-    float* __restrict__ partial) {
+    float* __restrict__ partial, const uint8_t* __restrict__ gate = nullptr,
+    int64_t ldgate = 0) {
   __shared__ float red[4][kReluMaxK4 * 64 * 4];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int64_t r0 = static_cast<int64_t>(blockIdx.x) * rows_per_block;
@@ -124,7 +131,8 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
 #pragma unroll 2
   for (int64_t r = r0 + w; r < r1; r += 4) {
     const float* gr = gY + r * ldg;
-    const float* yr = MASK ? Y + r * ldy : nullptr;
+    const float* yr = (MASK && !GATE) ? Y + r * ldy : nullptr;
+    const uint8_t* gt = GATE ? gate + r * ldgate : nullptr;
     float* orow = MASK ? g_out + r * ldo : nullptr;
 #pragma unroll
     for (int p = 0; p < kReluMaxK4; ++p) {
@@ -136,7 +144,10 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
           for (int e = 0; e < 4; ++e)
             if (c + e < K) {
               float o = gr[c + e];
-              if constexpr (MASK) {
+              if constexpr (GATE) {
+                o = gate_apply(o, gt[c + e]);
+                orow[c + e] = o;
+              } else if constexpr (MASK) {
                 o = yr[c + e] > 0.f ? o : 0.f;
                 orow[c + e] = o;
               }
@@ -145,7 +156,12 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
           continue;
         }
         float4 o = *reinterpret_cast<const float4*>(gr + c);
-        if constexpr (MASK) {
+        if constexpr (GATE) {
+          const uint32_t gv = *reinterpret_cast<const uint32_t*>(gt + c);
+          o = make_float4(gate_apply(o.x, gv & 0xffu), gate_apply(o.y, (gv >> 8) & 0xffu),
+                          gate_apply(o.z, (gv >> 16) & 0xffu), gate_apply(o.w, gv >> 24));
+          *reinterpret_cast<float4*>(orow + c) = o;
+        } else if constexpr (MASK) {
           const float4 yv = *reinterpret_cast<const float4*>(yr + c);
           o = make_float4(yv.x > 0.f ? o.x : 0.f, yv.y > 0.f ? o.y : 0.f,
                           yv.z > 0.f ? o.z : 0.f, yv.w > 0.f ? o.w : 0.f);
@@ -154,7 +170,10 @@ __global__ __launch_bounds__(256) void relu_backward_kernel(
         acc[p][0] += o.x; acc[p][1] += o.y; acc[p][2] += o.z; acc[p][3] += o.w;
       } else {
         float o = gr[c];
-        if constexpr (MASK) {
+        if constexpr (GATE) {
+          o = gate_apply(o, gt[c]);
+          orow[c] = o;
+        } else if constexpr (MASK) {
           o = yr[c] > 0.f ? o : 0.f;
           orow[c] = o;
         }
@@ -316,11 +335,12 @@ gcg_status gcg_relu_backward_f32_workspace_bytes(int64_t M, int64_t K, size_t* b
 
 namespace {
 
-// shared by gcg_relu_backward_f32 (MASK) and gcg_column_sum_f32 (no mask)
+// shared by gcg_relu_backward_f32 (MASK: Y), gcg_relu_backward_gate_f32 (MASK: gate bytes)
+// and gcg_column_sum_f32 (no mask)
 gcg_status relu_colsum(const char* fn, bool mask, int64_t M, int64_t K, const float* gY,
                        int64_t ldg, const float* Y, int64_t ldy, float* g_out, int64_t ldo,
                        float* bias_grad, void* workspace, size_t workspace_bytes,
-                       gcg_stream_t stream) {
+                       gcg_stream_t stream, const uint8_t* gate = nullptr, int64_t ldgate = 0) {
   if (M < 0 || K < 0 || K > 64 * 4 * kReluMaxK4)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld K=%lld (K <= %d)", fn,
                 static_cast<long long>(M), static_cast<long long>(K), 64 * 4 * kReluMaxK4);
@@ -329,6 +349,13 @@ gcg_status relu_colsum(const char* fn, bool mask, int64_t M, int64_t K, const fl
     if (bias_grad != nullptr && K > 0)
       GCG_HIP_CHECK(hipMemsetAsync(bias_grad, 0, sizeof(float) * K, st));
     return GCG_OK;
+  }
+  const bool use_gate = mask && gate != nullptr;
+  if (use_gate) {  // the gate stands in for Y
+    if (ldgate < K || ldgate % 4 != 0 || !aligned(gate, 4))
+      return fail(GCG_ERR_MISALIGNED, "%s: gate needs ldgate >= K, ldgate %% 4 == 0, 4-B base", fn);
+    Y = gY;
+    ldy = ldg;
   }
   if (gY == nullptr || (mask && (Y == nullptr || g_out == nullptr)) ||
       (!mask && bias_grad == nullptr))
@@ -350,13 +377,17 @@ gcg_status relu_colsum(const char* fn, bool mask, int64_t M, int64_t K, const fl
     return fail(GCG_ERR_MISALIGNED, "%s: K > %d needs 16-B rows (ld %% 4 == 0)", fn,
                 64 * kReluMaxK4);
   const dim3 grid(static_cast<unsigned>(n_blocks));
-#define GCG_RELU_LAUNCH(V, MK)                                                                  \
-  hipLaunchKernelGGL((relu_backward_kernel<V, MK>), grid, dim3(256), 0, st, M, int(K), rpb, gY, \
-                     ldg, Y, ldy, g_out, ldo, part)
+#define GCG_RELU_LAUNCH(V, MK, GT)                                                              \
+  hipLaunchKernelGGL((relu_backward_kernel<V, MK, GT>), grid, dim3(256), 0, st, M, int(K), rpb,  \
+                     gY, ldg, Y, ldy, g_out, ldo, part, gate, ldgate)
   if (vec) {
-    if (mask) GCG_RELU_LAUNCH(4, true); else GCG_RELU_LAUNCH(4, false);
+    if (use_gate) GCG_RELU_LAUNCH(4, true, true);
+    else if (mask) GCG_RELU_LAUNCH(4, true, false);
+    else GCG_RELU_LAUNCH(4, false, false);
   } else {
-    if (mask) GCG_RELU_LAUNCH(1, true); else GCG_RELU_LAUNCH(1, false);
+    if (use_gate) GCG_RELU_LAUNCH(1, true, true);
+    else if (mask) GCG_RELU_LAUNCH(1, true, false);
+    else GCG_RELU_LAUNCH(1, false, false);
   }
 #undef GCG_RELU_LAUNCH
   GCG_HIP_CHECK(hipGetLastError());
@@ -376,6 +407,16 @@ gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t 
                                  gcg_stream_t stream) {
   return relu_colsum("gcg_relu_backward_f32", true, M, K, gY, ldg, Y, ldy, g_out, ldo, bias_grad,
                      workspace, workspace_bytes, stream);
+}
+
+gcg_status gcg_relu_backward_gate_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
+                                      const uint8_t* gate, int64_t ldgate, float* g_out,
+                                      int64_t ldo, float* bias_grad, void* workspace,
+                                      size_t workspace_bytes, gcg_stream_t stream) {
+  if (M > 0 && K > 0 && gate == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "gcg_relu_backward_gate_f32: gate is NULL");
+  return relu_colsum("gcg_relu_backward_gate_f32", true, M, K, gY, ldg, nullptr, 0, g_out, ldo,
+                     bias_grad, workspace, workspace_bytes, stream, gate, ldgate);
 }
 
 gcg_status gcg_column_sum_f32(int64_t M, int64_t K, const float* X, int64_t ldx, float* out,

@@ -404,7 +404,10 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
     for (int e = 0; e < 4; ++e) m = fmaxf(m, v[i][e]);
   }
   m = reduce16_max<64>(m);
-  const int y = labels ? labels[row] : -1;
+  // a label outside [0, N) gets a NaN loss (never a silent wrong class); -1 = no labels
+  int y = labels ? labels[row] : -1;
+  const bool bad_y = labels != nullptr && (y < 0 || y >= N);
+  y = bad_y ? -1 : y;
   float s = 0.f, x = 0.f;
   int a = 0x7fffffff;
 #pragma unroll
@@ -419,9 +422,9 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
   s = reduce16_sum<64>(s);
   x = reduce16_sum<64>(x);
   a = reduce16_min<64>(a);
-  if (y >= 0 && lane == 0) {
-    loss_rows[row] = (m + logf(s)) - x;
-    if (correct_rows) correct_rows[row] = (a == y) ? 1.f : 0.f;
+  if (labels != nullptr && lane == 0) {
+    loss_rows[row] = bad_y ? std::numeric_limits<float>::quiet_NaN() : (m + logf(s)) - x;
+    if (correct_rows) correct_rows[row] = (!bad_y && a == y) ? 1.f : 0.f;
   }
   if (O == nullptr) return;  // loss / accuracy only
   if (scale_dev != nullptr) scale *= *scale_dev;
@@ -435,7 +438,7 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float p = expf(v[i][e] - m) * inv;
-      if (y >= 0) p = (p - ((c + e) == y ? 1.f : 0.f)) * scale;
+      if (labels != nullptr) p = (p - ((c + e) == y ? 1.f : 0.f)) * scale;
       o[e] = p;
     }
     if (vec && c + 3 < N) {

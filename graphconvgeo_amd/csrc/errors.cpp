@@ -1,4 +1,4 @@
-// errors.cpp -- per-thread last-error text and the version string of the C-ABI.
+// errors.cpp -- per-thread last-error text, the version string and the source hash of the C-ABI.
 #include <cstdarg>
 #include <cstdio>
 #include <string>
@@ -23,7 +23,12 @@ gcg_status fail(gcg_status st, const char* fmt, ...) {
 const char* last_error() { return g_last_error.c_str(); }
 }  // namespace gcg
 
+#ifndef GCG_SOURCE_HASH
+#define GCG_SOURCE_HASH "unknown"
+#endif
+
 extern "C" {
-const char* gcg_version(void) { return "0.1.0"; }
+const char* gcg_version(void) { return "0.2.0"; }
+const char* gcg_source_hash(void) { return GCG_SOURCE_HASH; }
 const char* gcg_last_error(void) { return gcg::last_error(); }
 }

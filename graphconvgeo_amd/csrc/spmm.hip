@@ -82,6 +82,26 @@ __device__ __forceinline__ float apply_act(float y, int act) {
   return act == GCG_ACT_RELU ? 0.5f * (y + fabsf(y)) : y;
 }
 
+// Rectify gate of a pre-activation x: Theano's relu(x) = 0.5*(x + |x|) has the gradient
+// 0.5*g*(1 + sgn(x)) (mlpconv.py:77 via lasagne rectify), i.e. g, g/2 or 0 for x > 0, x == 0,
+// x < 0. The byte keeps 2 * that factor: 2, 1, 0 (NaN -> 0). Read by gcg_relu_backward_gate_f32.
+__device__ __forceinline__ uint32_t gate_code(float x) {
+  return x > 0.0f ? 2u : (x == 0.0f ? 1u : 0u);
+}
+
+template <int VEC>
+__device__ __forceinline__ void store_gate(uint8_t* __restrict__ p, const Vec<VEC>& v) {
+  if constexpr (VEC == 4) {
+    *reinterpret_cast<uint32_t*>(p) = gate_code(v.x[0]) | (gate_code(v.x[1]) << 8) |
+                                      (gate_code(v.x[2]) << 16) | (gate_code(v.x[3]) << 24);
+  } else if constexpr (VEC == 2) {
+    *reinterpret_cast<uint16_t*>(p) =
+        static_cast<uint16_t>(gate_code(v.x[0]) | (gate_code(v.x[1]) << 8));
+  } else {
+    *p = static_cast<uint8_t>(gate_code(v.x[0]));
+  }
+}
+
 // Accumulate nonzeros [s, e) of one row into acc, storage order, U gathers in flight.
 template <int VEC, int NCH, int U>
 __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __restrict__ indices,
@@ -153,7 +173,8 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
-    float* __restrict__ ws, int64_t ldws, int xcd_remap) {
+    float* __restrict__ ws, int64_t ldws, int xcd_remap, uint8_t* __restrict__ gate,
+    int64_t ldgate) {
   // Optional XCD-aware mapping (experiment): blocks b and b + 8 share an XCD under the
   // observed round-robin dispatch, so block b takes task block (b % 8) * ceil(nb / 8) + b / 8
   // and each XCD walks one contiguous range of rows. Placement is speed-only, never correctness.
@@ -217,6 +238,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + b.x[q];
       }
+      if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], acc[k]);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = apply_act(acc[k].x[q], act);
       store_vec<VEC>(yrow + col[k], acc[k]);
@@ -232,7 +254,8 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(const int4* __restri
                                                             int64_t ldws, int K,
                                                             float* __restrict__ Y, int64_t ldy,
                                                             const float* __restrict__ bias,
-                                                            int act) {
+                                                            int act, uint8_t* __restrict__ gate,
+                                                            int64_t ldgate) {
   const int w = uniform(static_cast<int>(blockIdx.x) * kWavesPerBlock + (threadIdx.x >> 6));
   if (w >= n_long) return;
   const int c = static_cast<int>(blockIdx.y) * kWave + (threadIdx.x & (kWave - 1));
@@ -242,6 +265,7 @@ __global__ __launch_bounds__(kBlock) void spmm_fixup_kernel(const int4* __restri
   float acc = src[0];
   for (int s = 1; s < L.z; ++s) acc = acc + src[static_cast<int64_t>(s) * ldws];
   if (bias != nullptr) acc = acc + bias[c];
+  if (gate != nullptr) gate[static_cast<int64_t>(L.x) * ldgate + c] = static_cast<uint8_t>(gate_code(acc));
   Y[static_cast<int64_t>(L.x) * ldy + c] = apply_act(acc, act);
 }
 
@@ -265,6 +289,8 @@ struct LaunchArgs {
   float* ws;
   int64_t ldws;
   int64_t task_nnz;  // plan task size (0 = plan-less, one row per wave)
+  uint8_t* gate = nullptr;  // rectify gate bytes (nullable), row stride ldgate
+  int64_t ldgate = 0;
 };
 
 template <int VEC, int NCH, int U, int WPB>
@@ -273,7 +299,7 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   static const int xcd = env_int("GCG_XCD_REMAP");
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
-                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd);
+                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate, a.ldgate);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
@@ -365,6 +391,14 @@ gcg_status check_dense(const float* Z, int64_t ldz, float* Y, int64_t ldy, int64
   if (!aligned(Z, 4) || !aligned(Y, 4) || (bias && !aligned(bias, 4)))
     return fail(GCG_ERR_MISALIGNED, "Z/Y/bias not 4-byte aligned");
   if (act != GCG_ACT_NONE && act != GCG_ACT_RELU) return fail(GCG_ERR_INVALID_ARG, "bad act=%d", act);
+  return GCG_OK;
+}
+
+gcg_status check_gate(const uint8_t* gate, int64_t ldgate, int64_t K, int act) {
+  if (gate == nullptr) return GCG_OK;
+  if (act != GCG_ACT_RELU) return fail(GCG_ERR_INVALID_ARG, "gate needs act = GCG_ACT_RELU");
+  if (ldgate < K || ldgate % 4 != 0) return fail(GCG_ERR_INVALID_ARG, "ldgate=%lld: need >= K and %% 4 == 0", (long long)ldgate);
+  if (!aligned(gate, 4)) return fail(GCG_ERR_MISALIGNED, "gate not 4-byte aligned");
   return GCG_OK;
 }
 
@@ -477,17 +511,28 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz, const i
                             int64_t ldz, int64_t K, float* Y, int64_t ldy, const float* bias,
                             int act, const int32_t* out_rows, int64_t n_out,
                             gcg_stream_t stream) {
+  return gcg_spmm_csr_f32_gate(n_rows, n_cols, nnz, indptr, indices, vals, Z, ldz, K, Y, ldy,
+                               bias, act, out_rows, n_out, nullptr, 0, stream);
+}
+
+gcg_status gcg_spmm_csr_f32_gate(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                 const int32_t* indptr, const int32_t* indices,
+                                 const float* vals, const float* Z, int64_t ldz, int64_t K,
+                                 float* Y, int64_t ldy, const float* bias, int act,
+                                 const int32_t* out_rows, int64_t n_out, uint8_t* gate,
+                                 int64_t ldgate, gcg_stream_t stream) {
   if (n_rows < 0 || n_cols < 0 || nnz < 0 || n_rows > INT32_MAX || nnz > INT32_MAX)
     return fail(GCG_ERR_INVALID_ARG, "bad CSR shape n_rows=%lld n_cols=%lld nnz=%lld",
                 (long long)n_rows, (long long)n_cols, (long long)nnz);
   if (out_rows == nullptr) n_out = n_rows;
   if (n_out < 0 || n_out > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "bad n_out=%lld", (long long)n_out);
   if (gcg_status st = check_dense(Z, ldz, Y, ldy, K, bias, act)) return st;
+  if (gcg_status st = check_gate(gate, ldgate, K, act)) return st;
   if (n_out > 0 && indptr == nullptr) return fail(GCG_ERR_INVALID_ARG, "indptr is NULL");
   if (nnz > 0 && (indices == nullptr || vals == nullptr)) return fail(GCG_ERR_INVALID_ARG, "indices/vals NULL");
   if (n_out == 0 || K == 0) return GCG_OK;
   LaunchArgs a{nullptr, int(n_out), indptr, indices, vals, out_rows, Z, ldz, int(K), Y, ldy,
-               bias, act, nullptr, 0, 0};
+               bias, act, nullptr, 0, 0, gate, ldgate};
   return launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, nullptr, 0),
                      static_cast<hipStream_t>(stream));
 }
@@ -605,8 +650,19 @@ gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* in
                                     int64_t ldz, int64_t K, float* Y, int64_t ldy,
                                     const float* bias, int act, void* workspace,
                                     size_t workspace_bytes, gcg_stream_t stream) {
+  return gcg_spmm_csr_f32_planned_gate(plan, indptr, indices, vals, Z, ldz, K, Y, ldy, bias, act,
+                                       nullptr, 0, workspace, workspace_bytes, stream);
+}
+
+gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                         const int32_t* indices, const float* vals,
+                                         const float* Z, int64_t ldz, int64_t K, float* Y,
+                                         int64_t ldy, const float* bias, int act, uint8_t* gate,
+                                         int64_t ldgate, void* workspace,
+                                         size_t workspace_bytes, gcg_stream_t stream) {
   if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
   if (gcg_status st = check_dense(Z, ldz, Y, ldy, K, bias, act)) return st;
+  if (gcg_status st = check_gate(gate, ldgate, K, act)) return st;
   if (plan->n_out > 0 && indptr == nullptr) return fail(GCG_ERR_INVALID_ARG, "indptr is NULL");
   if (plan->nnz > 0 && (indices == nullptr || vals == nullptr)) return fail(GCG_ERR_INVALID_ARG, "indices/vals NULL");
   if (K == 0 || plan->n_tasks == 0) return GCG_OK;
@@ -619,12 +675,12 @@ gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* in
   float* ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
-               Y, ldy, bias, act, ws, ldws, plan->task_nnz};
+               Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate};
   if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
   if (plan->n_long > 0) {
     const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);
     hipLaunchKernelGGL(spmm_fixup_kernel, grid, dim3(kBlock), 0, st, plan->longs, plan->n_long,
-                       ws, ldws, int(K), Y, ldy, bias, act);
+                       ws, ldws, int(K), Y, ldy, bias, act, gate, ldgate);
     GCG_HIP_CHECK(hipGetLastError());
   }
   return GCG_OK;

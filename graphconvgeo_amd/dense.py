@@ -76,7 +76,10 @@ class _WeightCache:
             self._key = None
         else:
             self._buf.copy_(src)
-            self._key = key
+            # A copy recorded into a graph runs at every replay, before that replay's Adam
+            # update, while W._version never moves on a replay: a key stored here would let
+            # the next eager call reuse a copy one update behind. Forget it instead.
+            self._key = None if capturing else key
         return self._buf
 
 
@@ -292,6 +295,10 @@ class Projection:
 
 
 def _labels_i32(labels: torch.Tensor, M: int, N: int) -> torch.Tensor:
+    """int32 device labels. Their range is not checked here (that would synchronize, and the
+    call sits inside captured graphs): the kernels give a row whose label is outside [0, N)
+    a NaN loss, so the mean loss turns NaN instead of silently using a wrong class, and
+    MLPCONV.fit checks the host labels once."""
     _require_cuda(labels, "labels")
     if labels.numel() != M:
         raise ValueError(f"labels has {labels.numel()} entries for {M} rows")

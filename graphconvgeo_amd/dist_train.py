@@ -44,15 +44,21 @@ class GPUOps:
     """Rank-local kernels of the partitioned propagate (HIP). Tests inject CPU versions."""
 
     @staticmethod
-    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto"):
-        return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
+    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto", want_gate=False):
+        """Y, or (Y, gate) with the rectify gate bytes (sparse.spmm(gate=...)) if want_gate."""
+        if not want_gate:
+            return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
+        n_out = A.n_rows if rows is None else len(rows)
+        gate = gs.empty_gate(n_out, Z.shape[1], A.device)
+        return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode, gate=gate), gate
 
     @staticmethod
-    def relu_backward(gY, Y, bias_grad=True):
+    def relu_backward(gY, gate, bias_grad=True):
+        """Theano's rectify gradient (g, g/2, 0 for gate 2, 1, 0) + the bias gradient."""
         if gY.shape[1] <= 1024:
-            return gs.relu_backward(gY if gY.stride(-1) == 1 else gY.contiguous(), Y,
+            return gs.relu_backward(gY if gY.stride(-1) == 1 else gY.contiguous(), gate=gate,
                                     bias_grad=bias_grad)
-        g = gY * (Y > 0).to(gY.dtype)
+        g = gY * (gate.to(gY.dtype) * 0.5)
         return g, (g.sum(dim=0) if bias_grad else None)
 
     @staticmethod
@@ -71,22 +77,27 @@ class _PartitionedPropagate(torch.autograd.Function):
     @staticmethod
     def forward(ctx, Z_p, bias, part: RowPartitionedCSR, act, rows, mode, ops):
         operand = part.all_gather(Z_p.detach())
-        Y = ops.spmm(part.A, operand, bias=None if bias is None else bias.detach(), act=act,
-                     rows=rows, mode=mode)
+        b = None if bias is None else bias.detach()
+        gate = None
+        if act == "relu" and any(ctx.needs_input_grad[:2]):
+            Y, gate = ops.spmm(part.A, operand, bias=b, act=act, rows=rows, mode=mode,
+                               want_gate=True)
+        else:
+            Y = ops.spmm(part.A, operand, bias=b, act=act, rows=rows, mode=mode)
         ctx.part, ctx.act, ctx.rows, ctx.mode, ctx.ops = part, act, rows, mode, ops
         ctx.has_bias = bias is not None
         ctx.n_in = Z_p.shape[0]
-        ctx.save_for_backward(Y if act == "relu" else None)
+        ctx.save_for_backward(gate)
         return Y
 
     @staticmethod
     def backward(ctx, gY):
-        (Y,) = ctx.saved_tensors
+        (gate,) = ctx.saved_tensors
         want_bias = ctx.has_bias and ctx.needs_input_grad[1]
-        if Y is None:
+        if gate is None:
             g, g_bias = gY, (gY.sum(dim=0) if want_bias else None)
         else:
-            g, g_bias = ctx.ops.relu_backward(gY, Y, bias_grad=want_bias)
+            g, g_bias = ctx.ops.relu_backward(gY, gate, bias_grad=want_bias)
         g_Z = None
         if ctx.needs_input_grad[0]:
             part = ctx.part
@@ -142,9 +153,10 @@ class RowPartitionedGCN:
         self.rows = gs.RowSelection(loc, self.device)
         self.y_p = torch.as_tensor(np.asarray(y)[idx[pos]].astype(np.int32), device=self.device)
         F = X.shape[1]
-        gen = torch.Generator().manual_seed(seed)
-        w1 = _glorot_uniform(F, hidden, gen) if W1 is None else torch.as_tensor(np.asarray(W1))
-        w2 = _glorot_uniform(hidden, n_classes, gen) if W2 is None else torch.as_tensor(np.asarray(W2))
+        rng = np.random.RandomState(seed)  # every rank draws the same W1, W2 (then broadcast)
+        w1 = torch.as_tensor(_glorot_uniform(F, hidden, rng) if W1 is None else np.asarray(W1))
+        w2 = torch.as_tensor(_glorot_uniform(hidden, n_classes, rng) if W2 is None
+                             else np.asarray(W2))
         self.W1 = torch.nn.Parameter(w1.to(self.device, torch.float32).contiguous())
         self.b1 = torch.nn.Parameter(torch.zeros(hidden, device=self.device))
         self.W2 = torch.nn.Parameter(w2.to(self.device, torch.float32).contiguous())

@@ -5,7 +5,8 @@ Reference (Lasagne `Layer` subclasses, Theano graph, host CPU):
     SparseConvolutionDenseLayer(incoming, H=None, num_units, W=GlorotUniform(),
                                 b=Constant(0.), nonlinearity=rectify)          mlpconv.py:59-77
         get_output_for(X) = nonlinearity(S.dot(H, S.dot(X, W)) + b);  X must be sparse
-    ConvolutionDenseLayer(incoming, H=None, num_units, nonlinearity=softmax)   mlpconv.py:79-95
+    ConvolutionDenseLayer(incoming, H=None, num_units, W=GlorotUniform(), b=Constant(0.),
+                          nonlinearity=rectify)  (MLPCONV passes softmax)   mlpconv.py:79-95
         get_output_for(h, target_indices=idx) = nonlinearity((S.dot(H, T.dot(h, W)) + b)[idx])
 
 Here: torch modules with the same constructor arguments and `get_output_for` /
@@ -18,8 +19,13 @@ S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H for the symmetric H; CSR(X^T) built on
 device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
 
 `GraphConvLayer` is the name BASELINE.json's north_star uses; it is the generic form.
-Differences from Theano, by design: at a pre-activation of exactly 0.0 Theano's relu
-gradient is 0.5*g (d/dx 0.5(x+|x|)); here it is 0 (the mask is output > 0).
+Rectify is Theano's 0.5*(x+|x|) in the forward, and its gradient 0.5*g*(1+sgn(x)) in the
+backward -- g/2 at an exactly-zero pre-activation -- from the gate bytes the SpMM epilogue
+writes (sparse.spmm(gate=...)).
+
+Weights default to Lasagne's GlorotUniform drawn from numpy's global stream (W1 then W2 in
+MLPCONV, as the reference's DenseLayer constructors draw them), so `np.random.seed(77)`
+before the model (tensormain.py:227) starts from the reference's weights.
 """
 from __future__ import annotations
 
@@ -36,10 +42,26 @@ from . import sparse as gs
 _FUSED_ACTS = {"rectify": "relu", "relu": "relu"}
 
 
-def _glorot_uniform(fan_in: int, fan_out: int, generator=None) -> torch.Tensor:
-    """lasagne.init.GlorotUniform(gain=1.0) for a DenseLayer W of shape (num_inputs, num_units)."""
-    a = float(np.sqrt(6.0 / (fan_in + fan_out)))
-    return (torch.rand((fan_in, fan_out), generator=generator, dtype=torch.float32) * 2 - 1) * a
+def _glorot_uniform(fan_in: int, fan_out: int, rng=None) -> np.ndarray:
+    """lasagne.init.GlorotUniform(gain=1.0).sample((num_inputs, num_units)), the default W of
+    a Lasagne DenseLayer (mlpconv.py:208; ConvolutionDenseLayer's default at mlpconv.py:214):
+    std = gain * sqrt(2 / ((n1 + n2) * receptive_field_size)); Uniform(std=std) draws
+    uniform(low=0 - sqrt(3)*std, high=0 + sqrt(3)*std, size) from lasagne.random.get_rng(),
+    which is numpy's global stream unless set, then floatX (float32). [recalled Lasagne 0.2;
+    Lasagne is not importable here, so this draw order is parity-unpinned.]
+
+    rng: None -> numpy's global stream (np.random; main_mlpconv seeds it with
+    np.random.seed(77), tensormain.py:227, before MLPCONV draws W1 then W2), an int seed, or a
+    numpy RandomState / Generator."""
+    if rng is None:
+        rng = np.random.mtrand._rand
+    elif isinstance(rng, (int, np.integer)):
+        rng = np.random.RandomState(int(rng))
+    n1, n2 = int(fan_in), int(fan_out)
+    receptive_field_size = np.prod(())  # 1.0: DenseLayer weights are 2-D
+    std = 1.0 * np.sqrt(2.0 / ((n1 + n2) * receptive_field_size))
+    a, b = 0.0 - np.sqrt(3) * std, 0.0 + np.sqrt(3) * std
+    return np.asarray(rng.uniform(low=a, high=b, size=(n1, n2)), dtype=np.float32)
 
 
 def _as_tensor(x, shape, device) -> torch.Tensor:
@@ -90,27 +112,35 @@ class _CSRMatMul(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, Z, bias, A: gs.DeviceCSR, act, rows, mode):
-        Y = gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
+        gate = None
+        if act == "relu" and any(ctx.needs_input_grad[:2]):
+            # rectify gate (2/1/0 for pre-activation > 0, == 0, < 0) written by the SpMM
+            # epilogue: Theano's relu gradient is g/2 at an exact-zero pre-activation
+            # (e.g. an isolated node with an empty X row and b = 0), which the output
+            # alone cannot tell from a negative one
+            n_out = A.n_rows if rows is None else len(rows)
+            gate = gs.empty_gate(n_out, Z.shape[1], A.device)
+        Y = gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode, gate=gate)
         ctx.A, ctx.act, ctx.rows, ctx.mode = A, act, rows, mode
         ctx.has_bias = bias is not None
-        ctx.save_for_backward(Y if act == "relu" else None)
+        ctx.save_for_backward(gate)
         return Y
 
     @staticmethod
     def backward(ctx, gY):
         A, rows = ctx.A, ctx.rows
-        (Y,) = ctx.saved_tensors
+        (gate,) = ctx.saved_tensors
         want_bias = ctx.has_bias and ctx.needs_input_grad[1]
-        if Y is not None and gY.shape[1] <= 1024:
-            # rectify mask and bias gradient in one pass (gcg_relu_backward_f32)
-            g, g_bias = gs.relu_backward(gY.contiguous() if gY.stride(-1) != 1 else gY, Y,
-                                         bias_grad=want_bias)
-        elif Y is None:
+        if gate is not None and gY.shape[1] <= 1024:
+            # Theano rectify gradient and bias gradient in one pass (gcg_relu_backward_gate_f32)
+            g, g_bias = gs.relu_backward(gY.contiguous() if gY.stride(-1) != 1 else gY,
+                                         gate=gate, bias_grad=want_bias)
+        elif gate is None:
             g = gY
             g_bias = (gs.column_sum(gY) if gY.shape[1] <= 1024 else gY.sum(dim=0)) \
                 if want_bias else None
         else:
-            g = gY * (Y > 0).to(gY.dtype)
+            g = gY * (gate.to(gY.dtype) * 0.5)
             g_bias = g.sum(dim=0) if want_bias else None
         g_Z = None
         if ctx.needs_input_grad[0]:
@@ -166,7 +196,7 @@ class GraphConvLayer(nn.Module):
 
     def __init__(self, incoming=None, H=None, num_units: int = None, W=None, b=0.0,
                  nonlinearity="rectify", device: Union[str, torch.device] = "cuda",
-                 mode: str = "auto", require_sparse_input: bool = False, generator=None,
+                 mode: str = "auto", require_sparse_input: bool = False, rng=None,
                  in_features: Optional[int] = None):
         super().__init__()
         if num_units is None:
@@ -179,7 +209,7 @@ class GraphConvLayer(nn.Module):
         self.H = _as_device_csr(H, self.device)
         if self.H.symmetric is None:
             self.H.symmetric = False  # transpose built on demand unless declared symmetric
-        w = _glorot_uniform(self.num_inputs, self.num_units, generator) if W is None else W
+        w = _glorot_uniform(self.num_inputs, self.num_units, rng) if W is None else W
         self.W = nn.Parameter(_as_tensor(w, (self.num_inputs, self.num_units), self.device))
         if b is None:
             self.b = None
@@ -229,6 +259,9 @@ class SparseConvolutionDenseLayer(GraphConvLayer):
 class ConvolutionDenseLayer(GraphConvLayer):
     """mlpconv.py:79-95: nonlinearity((S.dot(H, T.dot(h, W)) + b)[target_indices]).
 
+    The default nonlinearity is rectify, Lasagne DenseLayer's default (the class only adds H);
+    MLPCONV passes softmax explicitly (mlpconv.py:214-217).
+
     order: "reference" -- transform then propagate, as mlpconv.py:88-90 (default);
            "propagate_first" -- ((H . h)[target_indices]) . W + b: the SpMM runs at the
            input width K instead of num_units C and only for the target rows, and its
@@ -238,7 +271,7 @@ class ConvolutionDenseLayer(GraphConvLayer):
     """
 
     def __init__(self, incoming=None, H=None, num_units=None, W=None, b=0.0,
-                 nonlinearity="softmax", order: str = "reference", **kw):
+                 nonlinearity="rectify", order: str = "reference", **kw):
         super().__init__(incoming, H=H, num_units=num_units, W=W, b=b,
                          nonlinearity=nonlinearity, **kw)
         if order not in ("reference", "propagate_first", "auto"):
@@ -274,14 +307,14 @@ class SparseInputDenseLayer(nn.Module):
 
     def __init__(self, incoming=None, num_units: int = None, W=None, b=0.0,
                  nonlinearity="rectify", device: Union[str, torch.device] = "cuda",
-                 mode: str = "auto", generator=None, in_features: Optional[int] = None):
+                 mode: str = "auto", rng=None, in_features: Optional[int] = None):
         super().__init__()
         if num_units is None:
             raise ValueError("num_units is required")
         self.device = torch.device(device)
         self.num_inputs = in_features if in_features is not None else _num_inputs(incoming)
         self.num_units = int(num_units)
-        w = _glorot_uniform(self.num_inputs, self.num_units, generator) if W is None else W
+        w = _glorot_uniform(self.num_inputs, self.num_units, rng) if W is None else W
         self.W = nn.Parameter(_as_tensor(w, (self.num_inputs, self.num_units), self.device))
         if b is None:
             self.b = None
@@ -310,7 +343,7 @@ class GCN(nn.Module):
     """
 
     def __init__(self, H, X, in_features: int, hidden: int, n_classes: int,
-                 device="cuda", W1=None, W2=None, mode: str = "auto", generator=None):
+                 device="cuda", W1=None, W2=None, mode: str = "auto", rng=None):
         super().__init__()
         self.device = torch.device(device)
         Hd = _as_device_csr(H, self.device)
@@ -319,10 +352,10 @@ class GCN(nn.Module):
         self.X = _as_device_csr(X, self.device)
         self.l_hid1 = SparseConvolutionDenseLayer(in_features, H=Hd, num_units=hidden, W=W1,
                                                   nonlinearity="rectify", device=self.device,
-                                                  mode=mode, generator=generator)
+                                                  mode=mode, rng=rng)
         self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=n_classes,
                                            W=W2, nonlinearity="softmax", device=self.device,
-                                           mode=mode, generator=generator)
+                                           mode=mode, rng=rng)
 
     def forward(self, target_indices):
         h = self.l_hid1(self.X)

@@ -120,9 +120,9 @@ class MLPCONV:
 
     # -- model --------------------------------------------------------------------------
     def _build(self, in_size: int, out_size: int, H):
-        gen = None
-        if self.seed is not None:
-            gen = torch.Generator().manual_seed(self.seed)
+        # Lasagne GlorotUniform draws W1 then W2 from numpy's global stream (mlpconv.py:205-217;
+        # main_mlpconv seeds it, tensormain.py:227); `seed` gives a private stream instead
+        rng = None if self.seed is None else np.random.RandomState(self.seed)
         Hd = H if isinstance(H, gs.DeviceCSR) else gs.DeviceCSR.from_scipy(H, self.device)
         if Hd.symmetric is None:
             Hd.symmetric = True  # D^-1/2 (A+I) D^-1/2 of an undirected graph
@@ -131,10 +131,10 @@ class MLPCONV:
             W1, _b1, W2, _b2 = self.init_parameters
         self.l_hid1 = SparseConvolutionDenseLayer(in_size, H=Hd, num_units=self.hidden_layer_size,
                                                   W=W1, nonlinearity="rectify", device=self.device,
-                                                  mode=self.mode, generator=gen)
+                                                  mode=self.mode, rng=rng)
         self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=out_size,
                                            W=W2, nonlinearity=None, device=self.device,
-                                           mode=self.mode, generator=gen, order=self.order)
+                                           mode=self.mode, rng=rng, order=self.order)
         if self.init_parameters is not None:
             with torch.no_grad():
                 self.l_hid1.b.copy_(torch.as_tensor(self.init_parameters[1]))
@@ -180,6 +180,10 @@ class MLPCONV:
     def fit(self, X, train_indices, dev_indices, test_indices, Y, H):
         """mlpconv.py:152-318 (full-batch epochs, validation every report_k_epoch)."""
         Y = np.asarray(Y)
+        if Y.ndim != 1 or not np.issubdtype(Y.dtype, np.integer):
+            raise ValueError("Y must be a 1-D integer label array (complete_prob is out of scope)")
+        if Y.size and int(Y.min()) < 0:
+            raise ValueError("labels must be >= 0 (class ids, data.py:399-432)")
         out_size = int(np.max(Y)) + 1
         in_size = X.shape[1]
         if self.hidden_layer_size is None:
@@ -224,7 +228,20 @@ class MLPCONV:
                 for p, b in zip(self.params, best_params):
                     p.copy_(b)
         if self.model_file:
-            torch.save([p.detach().cpu() for p in self.params], self.model_file)
+            # the reference always pickles the best params (mlpconv.py:310-313); here only on
+            # request: model_file="reference" writes its path, anything else is a path
+            path = self.model_file
+            if path == "reference":
+                path = (f"./data/Xshape1_{in_size}_hidden_{self.hidden_layer_size}_regul_"
+                        f"{self.regul_coefs[0]}_drop_{self.dropout_coefs[0]}.pkl")
+            log.info("storing best parameters in %s ...", path)
+            torch.save([p.detach().cpu() for p in self.params], path)
+            self.model_path = path
+        # final dev evaluation with the restored best parameters (mlpconv.py:316-318)
+        with torch.no_grad():
+            l_val, a_val = self._loss_acc(self.rows["dev"], y_dev)
+        self.best_dev_loss, self.best_dev_acc = float(l_val), float(a_val)
+        log.info("Best dev acc: %f", self.best_dev_acc)
         return self
 
     def _make_train_step(self, opt: LasagneAdam, y_train: torch.Tensor):
@@ -293,7 +310,11 @@ class MLPCONV:
         _loss, acc = self._loss_acc(rows, y)
         return float(acc)
 
-    def score(self, dataset_partition, y_true):
+    def score(self, X, dataset_partition, y_true):
+        """mlpconv.py:348-349 `score(X, dataset_partition, y_true)`. The reference forwards all
+        three arguments to the two-argument accuracy() -- a TypeError there; this returns what
+        it evidently intends: the accuracy on the partition (X is the model's own input, kept
+        for the signature)."""
         return self.accuracy(dataset_partition, y_true)
 
     def get_params(self):

@@ -366,9 +366,17 @@ def empty_dense(n: int, k: int, device, pad_to: int = 4) -> torch.Tensor:
     return buf[:, :k] if ld != k else buf
 
 
+def empty_gate(n: int, k: int, device) -> torch.Tensor:
+    """[n, k] uint8 view of an [n, round4(k)] buffer: the rectify gate of spmm(gate=...)."""
+    ld = (k + 3) // 4 * 4
+    buf = torch.empty((n, ld), dtype=torch.uint8, device=device)
+    return buf[:, :k] if ld != k else buf
+
+
 def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
          act: Optional[str] = None, rows=None, mode: str = "auto",
-         out: Optional[torch.Tensor] = None, task_nnz: int = 0) -> torch.Tensor:
+         out: Optional[torch.Tensor] = None, task_nnz: int = 0,
+         gate: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Y = act(A . Z + bias)[rows] on the GPU (S.dot of mlpconv.py:71,73,90 + epilogue).
 
     mode  'auto'    : 'ordered' unless the longest row could outlast the launch, then 'fast'
@@ -377,6 +385,8 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
           'rowwise' : plan-less, one wave per output row -> bitwise scipy float32
     rows : None | RowSelection | int array -- output row subset (target_indices).
            A plain array/tensor runs plan-less (no plan to cache).
+    gate : optional uint8 [n_out, K] (empty_gate) receiving the rectify gate 2/1/0 of every
+           pre-activation (> 0, == 0, < 0) for Theano's rectify gradient (act='relu' only).
     """
     if not isinstance(A, DeviceCSR):
         raise ValueError("Input for this layer must be sparse")
@@ -417,6 +427,17 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         _same_device(out, A, "out")
         if out.shape != (n_out, K) or out.dtype != torch.float32 or (K > 1 and out.stride(1) != 1):
             raise ValueError(f"out must be float32 [{n_out}, {K}] with unit column stride")
+    ldg = 0
+    if gate is not None:
+        _require_cuda(gate, "gate")
+        _same_device(gate, A, "gate")
+        if ACTS[act] != GCG_ACT_RELU:
+            raise ValueError("gate needs act='relu'")
+        if gate.dtype != torch.uint8 or gate.shape != (n_out, K) or (K > 1 and gate.stride(1) != 1):
+            raise ValueError(f"gate must be uint8 [{n_out}, {K}] with unit column stride")
+        ldg = gate.stride(0) if n_out > 1 else (K + 3) // 4 * 4
+        if ldg % 4 or gate.data_ptr() % 4:
+            raise ValueError("gate needs a 4-B aligned base and row stride % 4 == 0 (empty_gate)")
     if n_out == 0 or K == 0:
         return out
     ldz = Z.stride(0) if Z.shape[0] > 1 else max(K, 1)
@@ -427,15 +448,15 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         mode = "ordered" if A.max_row_nnz() * AUTO_SPLIT_RATIO <= max(A.nnz, 1) else "fast"
     with torch.cuda.device(A.device):
         if mode == "rowwise":
-            call("gcg_spmm_csr_f32", A.n_rows, A.n_cols, A.nnz, _ptr(A.indptr), _ptr(A.indices),
-                 _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(rows_dev),
-                 n_out, stream)
+            call("gcg_spmm_csr_f32_gate", A.n_rows, A.n_cols, A.nnz, _ptr(A.indptr),
+                 _ptr(A.indices), _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc,
+                 _ptr(rows_dev), n_out, _ptr(gate), ldg, stream)
         else:
             plan = A.plan(sel, ordered=(mode == "ordered"), task_nnz=task_nnz)
             ws = plan.workspace(K)
-            call("gcg_spmm_csr_f32_planned", plan.handle, _ptr(A.indptr), _ptr(A.indices),
-                 _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(ws),
-                 0 if ws is None else ws.numel() * 4, stream)
+            call("gcg_spmm_csr_f32_planned_gate", plan.handle, _ptr(A.indptr), _ptr(A.indices),
+                 _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(gate), ldg,
+                 _ptr(ws), 0 if ws is None else ws.numel() * 4, stream)
     return out
 
 
@@ -471,13 +492,24 @@ def column_sum(X: torch.Tensor) -> torch.Tensor:
     return out
 
 
-def relu_backward(gY: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor] = None,
-                  bias_grad: bool = True):
-    """(g, db): g = gY where Y > 0 else 0 and db = column sums of g, one pass
-    (gcg_relu_backward_f32; the grad of rectify(. + b), mlpconv.py:75-77). out may be gY."""
+def relu_backward(gY: torch.Tensor, Y: Optional[torch.Tensor] = None,
+                  out: Optional[torch.Tensor] = None, bias_grad: bool = True,
+                  gate: Optional[torch.Tensor] = None):
+    """(g, db) and db = column sums of g, one pass (the grad of rectify(. + b),
+    mlpconv.py:75-77). With `gate` (the bytes spmm(gate=...) wrote): Theano's rule
+    g = gY, gY/2, 0 for a pre-activation > 0, == 0, < 0 (gcg_relu_backward_gate_f32);
+    with Y only: g = gY where Y > 0 else 0 (gcg_relu_backward_f32). out may be gY."""
     _require_cuda(gY, "gY")
-    _require_cuda(Y, "Y")
     M, K = gY.shape
+    if gate is not None:
+        _require_cuda(gate, "gate")
+        if gate.dtype != torch.uint8 or gate.shape != (M, K) or (K > 1 and gate.stride(1) != 1):
+            raise ValueError("gate must be uint8 [M, K] with unit column stride")
+        ldgate = gate.stride(0) if M > 1 else (K + 3) // 4 * 4
+        if ldgate % 4 or gate.data_ptr() % 4:
+            raise ValueError("gate needs a 4-B aligned base and row stride % 4 == 0")
+        Y = gY  # shape/stride checks below apply to the gradient only
+    _require_cuda(Y, "Y")
     if Y.shape != (M, K):
         raise ValueError("gY and Y must have the same shape")
     if out is None:
@@ -502,8 +534,12 @@ def relu_backward(gY: torch.Tensor, Y: torch.Tensor, out: Optional[torch.Tensor]
         if K > 1 and t.stride(1) != 1:
             raise ValueError("relu_backward operands need unit column stride")
     with torch.cuda.device(gY.device):
-        call("gcg_relu_backward_f32", M, K, _ptr(gY), ld(gY), _ptr(Y), ld(Y), _ptr(out), ld(out),
-             _ptr(db), _ptr(ws), ws.numel() * 4, _stream_handle(gY.device))
+        if gate is not None:
+            call("gcg_relu_backward_gate_f32", M, K, _ptr(gY), ld(gY), _ptr(gate), ldgate,
+                 _ptr(out), ld(out), _ptr(db), _ptr(ws), ws.numel() * 4, _stream_handle(gY.device))
+        else:
+            call("gcg_relu_backward_f32", M, K, _ptr(gY), ld(gY), _ptr(Y), ld(Y), _ptr(out),
+                 ld(out), _ptr(db), _ptr(ws), ws.numel() * 4, _stream_handle(gY.device))
     return out, db
 
 

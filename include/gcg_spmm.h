@@ -64,6 +64,9 @@ enum { GCG_ACT_NONE = 0, GCG_ACT_RELU = 1 };
 
 /* Library version, "major.minor.patch". */
 const char* gcg_version(void);
+/* Content hash of the sources the library was built from (graphconvgeo_amd/_build.py
+ * source_hash); the Python binding refuses a library whose hash differs from the tree's. */
+const char* gcg_source_hash(void);
 /* Text of the last error raised on this host thread ("" if none). */
 const char* gcg_last_error(void);
 
@@ -112,6 +115,27 @@ gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* in
                                     size_t workspace_bytes, gcg_stream_t stream);
 
 /*
+ * The same two SpMMs with the rectify gate written beside Y (act must be GCG_ACT_RELU):
+ * gate[i][c] (uint8, row stride ldgate >= K, ldgate % 4 == 0, 4-B aligned base) = 2, 1 or 0
+ * for a pre-activation > 0, == 0 or < 0 (NaN: 0) -- twice the factor of Theano's rectify
+ * gradient 0.5 * (1 + sgn(x)) (relu = 0.5*(x+|x|), mlpconv.py:77). It replaces keeping the
+ * output for the backward mask, and unlike the output it tells an exact-zero pre-activation
+ * (gradient g/2) from a negative one (gradient 0). Consumed by gcg_relu_backward_gate_f32.
+ */
+gcg_status gcg_spmm_csr_f32_gate(int64_t n_rows, int64_t n_cols, int64_t nnz,
+                                 const int32_t* indptr, const int32_t* indices,
+                                 const float* vals, const float* Z, int64_t ldz, int64_t K,
+                                 float* Y, int64_t ldy, const float* bias, int act,
+                                 const int32_t* out_rows, int64_t n_out, uint8_t* gate,
+                                 int64_t ldgate, gcg_stream_t stream);
+gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                         const int32_t* indices, const float* vals,
+                                         const float* Z, int64_t ldz, int64_t K, float* Y,
+                                         int64_t ldy, const float* bias, int act, uint8_t* gate,
+                                         int64_t ldgate, void* workspace,
+                                         size_t workspace_bytes, gcg_stream_t stream);
+
+/*
  * Host-only planner (no device memory, no HIP calls): the task list the plan uses,
  * exposed for testing and for host-side tools. `tasks_host` receives n_tasks int32
  * quadruples {a, b, c, d}: d < 0 -> rows of positions [a, b); d >= 0 -> segment of
@@ -158,6 +182,17 @@ gcg_status gcg_relu_backward_f32(int64_t M, int64_t K, const float* gY, int64_t 
                                  const float* Y, int64_t ldy, float* g_out, int64_t ldo,
                                  float* bias_grad /*nullable*/, void* workspace,
                                  size_t workspace_bytes, gcg_stream_t stream);
+
+/*
+ * Theano's rectify backward from the gate bytes of gcg_spmm_*_gate, with the bias gradient:
+ * g = gY, gY/2 or 0 for gate 2, 1, 0 (the gradient of 0.5*(x+|x|) at x > 0, x == 0, x < 0),
+ * bias_grad as gcg_relu_backward_f32 (same workspace size). K <= 1024.
+ */
+gcg_status gcg_relu_backward_gate_f32(int64_t M, int64_t K, const float* gY, int64_t ldg,
+                                      const uint8_t* gate, int64_t ldgate, float* g_out,
+                                      int64_t ldo, float* bias_grad /*nullable*/,
+                                      void* workspace, size_t workspace_bytes,
+                                      gcg_stream_t stream);
 
 /*
  * Column sums out[c] = sum_r X[r][c] (the bias gradient of a dense projection, colsum of the

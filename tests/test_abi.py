@@ -26,7 +26,7 @@ def test_header_declares_expected_entry_points():
 
 
 def test_library_exports_every_declared_symbol(native_lib):
-    from graphconvgeo_amd import _native
+    from graphconvgeo_amd import _build, _native
     for name in declared_functions():
         assert hasattr(native_lib, name), name
         assert name in _native.SIGNATURES, f"{name} has no ctypes signature"
@@ -34,7 +34,8 @@ def test_library_exports_every_declared_symbol(native_lib):
                         text=True, check=True).stdout
     exported = set(re.findall(r"\bT (gcg_[a-z0-9_]+)$", nm, flags=re.M))
     assert set(declared_functions()) <= exported
-    assert _native.version() == "0.1.0"
+    assert _native.version() == "0.2.0"
+    assert _native.load().gcg_source_hash().decode() == _build.source_hash()
 
 
 def test_header_compiles_as_c():

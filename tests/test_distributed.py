@@ -123,15 +123,19 @@ class _CPUOps:
     """Test-only rank-local ops for the partitioned propagate: the CPU oracle."""
 
     @staticmethod
-    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto"):
+    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto", want_gate=False):
         from oracle import gcn_oracle as O
         r = None if rows is None else rows.host
         b = None if bias is None else bias.numpy()
-        return torch.from_numpy(O.spmm_f32(A, Z.numpy(), bias=b, act=act, rows=r))
+        if not want_gate:
+            return torch.from_numpy(O.spmm_f32(A, Z.numpy(), bias=b, act=act, rows=r))
+        pre = O.spmm_f32(A, Z.numpy(), bias=b, rows=r)
+        gate = (2 * (pre > 0) + (pre == 0)).astype(np.uint8)  # Theano rectify gradient x2
+        return torch.from_numpy(O.relu(pre)), torch.from_numpy(gate)
 
     @staticmethod
-    def relu_backward(gY, Y, bias_grad=True):
-        g = gY * (Y > 0).to(gY.dtype)
+    def relu_backward(gY, gate, bias_grad=True):
+        g = gY * (gate.to(gY.dtype) * 0.5)
         return g, (g.sum(dim=0) if bias_grad else None)
 
     @staticmethod

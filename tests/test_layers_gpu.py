@@ -101,7 +101,8 @@ def test_sparse_input_dense_layer(cuda):
     ref = O.spmm_f32(X, W, bias=b, act="relu")
     assert np.array_equal(out.detach().cpu().numpy(), ref)  # bitwise scipy fp32 + epilogue
     out.sum().backward()
-    g = (ref > 0).astype(np.float64)
+    pre = O.spmm_f32(X, W, bias=b)
+    g = 0.5 * (1.0 + np.sign(pre.astype(np.float64)))  # Theano rectify gradient
     gW = sps.csr_matrix(X, dtype=np.float64).T @ g
     assert np.abs(lay.W.grad.cpu().numpy() - gW).max() < 1e-5 * np.abs(gW).max()  # fp32 sums of ~10^3 terms
     with pytest.raises(ValueError, match="must be sparse"):

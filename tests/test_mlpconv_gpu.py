@@ -55,6 +55,8 @@ def test_mlpconv_api(cuda, tmp_path):
     assert np.array_equal(pred, proba.argmax(axis=1))
     acc = clf.accuracy("test", Y[test])
     assert abs(acc - float((pred == Y[test]).mean())) < 1e-6
+    assert clf.score(X, "test", Y[test]) == acc  # mlpconv.py:348 signature
+    assert 0.0 <= clf.best_dev_acc <= 1.0  # final dev evaluation, mlpconv.py:316-318
     assert (tmp_path / "best.pt").exists()
     with pytest.raises(ValueError):
         clf.predict("nope")
@@ -86,6 +88,10 @@ def test_mlpconv_hip_graph_equals_eager(cuda, order):
     a = MLPCONV(**kw).fit(X, train, dev, test, Y, H)
     b = MLPCONV(use_graph=True, **kw).fit(X, train, dev, test, Y, H)
     assert [h["train_loss"] for h in a.history] == [h["train_loss"] for h in b.history]
+    # validation runs eagerly between replays: it must see the weights of the latest replay
+    # (a padded-weight copy cached during capture would be one Adam step behind)
+    assert [h.get("val_loss") for h in a.history] == [h.get("val_loss") for h in b.history]
+    assert a.best_dev_acc == b.best_dev_acc
     for pa, pb in zip(a.get_params(), b.get_params()):
         assert np.array_equal(pa, pb)  # replayed graph == eager, bit for bit
 
@@ -104,3 +110,21 @@ def test_main_mlpconv_call_pattern(cuda):
     y_pred = clf.predict(dataset_partition='test')
     assert 0.0 <= acc <= 1.0 and y_pred.shape == (len(test),)
     assert acc > 1.5 / 6  # learns beyond chance on feature-correlated labels
+
+
+def test_default_init_is_lasagne_glorot_from_numpy_global_stream(cuda):
+    """init_parameters=None: W1 then W2 from np.random after np.random.seed(77), as
+    main_mlpconv seeds it (tensormain.py:227) before MLPCONV's DenseLayers draw them
+    (mlpconv.py:205-217). Parity unpinned: Lasagne is not importable here."""
+    H, X, Y, train, dev, test, _ = problem(n=1500, e=9000, f=120, k=16, c=5)
+    np.random.seed(77)
+    clf = MLPCONV(n_epochs=0, hidden_layer_size=16, device=cuda)
+    clf.fit(X, train, dev, test, Y, H)
+    rs = np.random.RandomState(77)
+    a1 = np.sqrt(3) * np.sqrt(2.0 / (120 + 16))
+    a2 = np.sqrt(3) * np.sqrt(2.0 / (16 + 5))
+    W1 = rs.uniform(-a1, a1, size=(120, 16)).astype(np.float32)
+    W2 = rs.uniform(-a2, a2, size=(16, 5)).astype(np.float32)
+    got = clf.get_params()
+    assert np.array_equal(got[0], W1) and np.array_equal(got[2], W2)
+    assert not got[1].any() and not got[3].any()  # b = Constant(0.)

@@ -157,3 +157,19 @@ def test_scatter_add_and_adam():
     p = {"w": np.ones(3)}
     new = O.adam_step(p, {"w": np.array([1.0, -1.0, 0.0])}, st)
     assert np.allclose(new["w"], [1 - 4e-3, 1 + 4e-3, 1.0])
+
+
+def test_glorot_uniform_is_lasagne_draw_order():
+    """layers._glorot_uniform restates lasagne.init.GlorotUniform().sample((n1, n2)):
+    uniform(-sqrt(3)*std, sqrt(3)*std) with std = sqrt(2/(n1+n2)) from numpy's global
+    stream, floatX'd; two consecutive layers draw W1 then W2 (mlpconv.py:205-217)."""
+    from graphconvgeo_amd.layers import _glorot_uniform
+    np.random.seed(77)
+    W1 = _glorot_uniform(50, 8)
+    W2 = _glorot_uniform(8, 3)
+    rs = np.random.RandomState(77)
+    e1 = rs.uniform(-np.sqrt(3) * np.sqrt(2 / 58), np.sqrt(3) * np.sqrt(2 / 58), (50, 8))
+    e2 = rs.uniform(-np.sqrt(3) * np.sqrt(2 / 11), np.sqrt(3) * np.sqrt(2 / 11), (8, 3))
+    assert W1.dtype == np.float32 and np.array_equal(W1, e1.astype(np.float32))
+    assert np.array_equal(W2, e2.astype(np.float32))
+    assert np.array_equal(_glorot_uniform(50, 8, 5), _glorot_uniform(50, 8, np.random.RandomState(5)))
