@@ -34,6 +34,7 @@ from graphconvgeo_amd import sparse as gs  # noqa: E402
 from graphconvgeo_amd.synth import CONFIGS, SEED, synthetic_graph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md:296, "~6.3 TB/s achievable"
 
 
 def spmm_bytes(n_rows: int, nnz: int, K: int) -> int:
@@ -57,9 +58,37 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
+def scipy_baseline(H, K: int, nnz_sample: int = 8_000_000, reps: int = 5) -> dict:
+    """The reference's own executor: S.dot(H, Z) (mlpconv.py:73) is scipy's `H @ Z`
+    (csr_matvecs, single-threaded whatever the host). Timed on a fixed row sample -- the
+    leading rows holding ~nnz_sample nonzeros -- against the full N x K dense operand:
+    1 warm-up, then the median of `reps` runs (time.perf_counter)."""
+    import scipy
+
+    n = H.shape[0]
+    stop = int(np.searchsorted(H.indptr, min(H.nnz, nnz_sample), side="left"))
+    blk = H[:max(stop, 1)]
+    Z = np.random.default_rng(SEED + 5).standard_normal((H.shape[1], K), dtype=np.float32)
+    blk @ Z  # warm-up
+    ts = []
+    for _ in range(max(reps, 3)):
+        t0 = time.perf_counter()
+        blk @ Z
+        ts.append(time.perf_counter() - t0)
+    t = float(np.median(ts))
+    return {"value": round(spmm_bytes(blk.shape[0], blk.nnz, K) / t / 1e9, 3), "unit": "GB/s",
+            "cores": 1, "kind": "reference",
+            "edges_per_s": round(blk.nnz / t, 1),
+            "sample": f"scipy {scipy.__version__} H[:{blk.shape[0]}] @ Z ({blk.nnz} nnz x K={K}, "
+                      f"Z {H.shape[1]} x {K}), 1 warm-up + median of {len(ts)} "
+                      f"({', '.join(f'{x:.2f}' for x in ts)} s), single-threaded scipy "
+                      f"csr_matvecs on {cpu_model()} ({os.cpu_count()} host cpus); "
+                      f"extrapolated whole graph: {H.nnz / (blk.nnz / t):.1f} s"}
+
+
 def cpu_baseline(H, K: int, budget_s: float) -> dict:
-    """The oracle (C port of scipy csr_matvecs, 1 thread) on a bounded row sample of the
-    same graph: consecutive row blocks of ~1M nonzeros until `budget_s` is spent."""
+    """Labelled extra: the oracle (C port of scipy csr_matvecs, 1 thread) on a bounded row
+    sample of the same graph: consecutive row blocks of ~1M nonzeros until `budget_s` is spent."""
     from oracle import gcn_oracle as O
 
     rng = np.random.default_rng(SEED + 5)
@@ -117,17 +146,139 @@ def cpu_multicore(H, K: int, budget_s: float) -> dict:
             "sample": f"rows [0, {blk.shape[0]}): {blk.nnz} nnz x K={K}, {reps} reps"}
 
 
+PROFILE_ROUNDS = ("r02", "r01")  # newest first
+
+
 def load_traffic(workload: str, per_launch_bytes: int):
-    """HBM bytes per launch from the committed rocprofv3 PMC summary of this workload."""
-    path = os.path.join(ROOT, "profiles", "r01", f"pmc_{workload}.json")
-    if not os.path.exists(path):
-        return None, None
-    try:
-        with open(path) as f:
-            rec = json.load(f)
-        return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
-    except (OSError, ValueError):
-        return None, None
+    """L2->fabric bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
+    MI355X_MICROARCH.md:298; Infinity-Cache hits included, so not DRAM-only bytes) from the
+    newest committed rocprofv3 PMC summary of this workload."""
+    for rnd in PROFILE_ROUNDS:
+        path = os.path.join(ROOT, "profiles", rnd, f"pmc_{workload}.json")
+        if not os.path.exists(path):
+            continue
+        try:
+            with open(path) as f:
+                rec = json.load(f)
+            return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
+        except (OSError, ValueError):
+            continue
+    return None, None
+
+
+def time_events(fn, reps: int, dev) -> float:
+    """Mean per-call ms of fn() with HIP events on the current stream (fn launches there)."""
+    stream = torch.cuda.current_stream(dev)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(reps)]
+    for a, b in evs:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize(dev)
+    return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+
+
+def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev) -> dict:
+    """SURVEY.md §8d second run: the same SpMM on the uniform-degree graph of the same size,
+    where no hub rows are served from the Infinity Cache -- the honest HBM-gather case."""
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
+    A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
+    g = torch.Generator(device=dev).manual_seed(SEED + 11)
+    Z = torch.randn((H.shape[0], K), generator=g, device=dev)
+    Y = gs.empty_dense(H.shape[0], K, dev)
+    eff = resolve_mode(A, mode)
+    gs.spmm(A, Z, out=Y, mode=eff)
+    gs.spmm(A, Z, out=Y, mode=eff)
+    k_ms = time_events(lambda: gs.spmm(A, Z, out=Y, mode=eff), reps, dev)
+    B = spmm_bytes(H.shape[0], H.nnz, K)
+    gbs = B / (k_ms * 1e-3) / 1e9
+    wl = f"{cfg.name}-{kind}-k{K}-{eff}"
+    traffic, src = load_traffic(wl, B)
+    rec = {"graph": kind, "mode": eff, "nnz_H": H.nnz, "kernel_ms": round(k_ms, 3),
+           "value": round(gbs, 1), "unit": "GB/s", "edges_per_s": round(H.nnz / (k_ms * 1e-3), 1),
+           "frac": round(gbs / HBM_PEAK_GBS, 4),
+           "frac_vs_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
+           "algorithmic_bytes_per_launch": B, "traffic": traffic}
+    if src:
+        rec["traffic_source"] = src
+    del A, Z, Y
+    return rec
+
+
+def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -> dict:
+    """BASELINE config 3: one MLPCONV epoch (mlpconv.py:293-295 -> f_train: 2-layer GCN
+    forward + backward + Lasagne Adam, tensormain.py:232-237) at Twitter-US scale on one GPU,
+    in the reference's layer-2 order and the propagate-first order; plus each SpMM of the
+    step timed alone (HIP events) with its edge-centric GB/s. Synthetic data (seed 77):
+    power-law graph, 64-nnz/row BoW X, 60 % of nodes as train targets drawn with
+    replacement (tensormain.py:226)."""
+    from graphconvgeo_amd.mlpconv import LasagneAdam, MLPCONV
+    from graphconvgeo_amd.synth import synthetic_features
+
+    cfg = CONFIGS[config]
+    t0 = time.perf_counter()
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges)
+    X = synthetic_features(cfg.n_nodes, cfg.n_features, nnz_per_row=64)
+    n, K, C = cfg.n_nodes, cfg.hidden, cfg.n_classes
+    rng = np.random.default_rng(SEED)
+    Y = rng.integers(0, C, size=n)
+    n_tr = int(0.6 * n)
+    train = rng.choice(n_tr, size=n_tr).astype(np.int32)
+    dev_idx = np.arange(n_tr, int(0.8 * n), dtype=np.int32)
+    test_idx = np.arange(int(0.8 * n), n, dtype=np.int32)
+    t_gen = time.perf_counter() - t0
+    out = {"config": cfg.name, "nodes": n, "edges": cfg.n_edges, "nnz_H": H.nnz, "nnz_X": X.nnz,
+           "F": cfg.n_features, "K": K, "C": C, "train_rows": int(train.size),
+           "data": "synthetic", "data_gen_s": round(t_gen, 1), "steps": steps, "warmup": warmup}
+    clf = None
+    for order in ("reference", "propagate_first"):
+        clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, order=order)
+        clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H and X
+        y_train = torch.as_tensor(Y[train].astype(np.int32), device=dev)
+        step = clf._make_train_step(LasagneAdam(clf.params), y_train)
+        for _ in range(warmup):
+            step()
+        torch.cuda.synchronize(dev)
+        t1 = time.perf_counter()
+        for _ in range(steps):
+            loss, _acc = step()
+        torch.cuda.synchronize(dev)
+        ms = (time.perf_counter() - t1) / max(steps, 1) * 1e3
+        out[order] = {"ms_per_step": round(ms, 3), "loss": round(float(loss), 5)}
+    # each SpMM of the step alone, on the last model's device operands
+    A, Xd = clf.l_hid1.H, clf.Xd
+    rows = clf.rows["train"]
+    g = torch.Generator(device=dev).manual_seed(SEED + 21)
+    Z1 = gs.empty_dense(n, K, dev).copy_(torch.randn((n, K), generator=g, device=dev))
+    G2 = gs.empty_dense(train.size, C, dev).copy_(torch.randn((train.size, C), generator=g, device=dev))
+    W1 = clf.l_hid1.W.detach()
+    b1 = clf.l_hid1.b.detach()
+    gate = gs.empty_gate(n, K, dev)
+    At = A.rows_transpose(rows)
+    nnz_t = int(np.diff(H.indptr)[train].sum())
+    ops = {
+        "X.W1 (mlpconv.py:71)": (lambda: gs.spmm(Xd, W1), spmm_bytes(n, X.nnz, K),
+                                 "W1 (12 MB) cache-resident"),
+        "rectify(H.Z1 + b1) + gate (mlpconv.py:73-77)": (
+            lambda: gs.spmm(A, Z1, bias=b1, act="relu", gate=gate), spmm_bytes(n, H.nnz, K), ""),
+        "(H.Z2 + b2)[train], C wide (mlpconv.py:90-94)": (
+            lambda: gs.spmm(A, Z1[:, :C], rows=rows), spmm_bytes(train.size, nnz_t, C), ""),
+        "(H[train])^T.G2, C wide (grad of mlpconv.py:90-94)": (
+            lambda: gs.spmm(At, G2), spmm_bytes(n, nnz_t, C), ""),
+        "H.g1 (grad of mlpconv.py:73)": (lambda: gs.spmm(A, Z1), spmm_bytes(n, H.nnz, K), ""),
+        "X^T.g (grad of mlpconv.py:71)": (lambda: Xd.tmatmul(Z1), spmm_bytes(cfg.n_features, X.nnz, K),
+                                          "dense Zipf-head columns on the MFMA GEMM"),
+    }
+    per = {}
+    for name, (fn, nbytes, note) in ops.items():
+        fn()
+        k_ms = time_events(fn, max(steps, 5), dev)
+        per[name] = {"ms": round(k_ms, 3), "GBps_edge_centric": round(nbytes / (k_ms * 1e-3) / 1e9, 1)}
+        if note:
+            per[name]["note"] = note
+    out["spmm"] = per
+    return out
 
 
 def resolve_mode(A, mode: str) -> str:
@@ -147,7 +298,12 @@ def main():
     ap.add_argument("--mode", default="auto", choices=list(gs.MODES))
     ap.add_argument("--task-nnz", type=int, default=0)
     ap.add_argument("--ld", type=int, default=0, help="row stride of Z/Y in floats (0 = K rounded to 4)")
-    ap.add_argument("--cpu-budget", type=float, default=12.0, help="seconds of CPU baseline")
+    ap.add_argument("--cpu-budget", type=float, default=6.0,
+                    help="seconds of the C-port CPU extra (the scipy baseline is a fixed sample)")
+    ap.add_argument("--no-variants", dest="variants", action="store_false",
+                    help="N = 1: skip the uniform-degree second run")
+    ap.add_argument("--no-train-step", dest="train_step", action="store_false",
+                    help="N = 1: skip the config-3 (Twitter-US) training-step measurement")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
@@ -176,6 +332,8 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group("gloo")
+        if dist.get_world_size() != world:
+            raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 
     cfg = CONFIGS[args.config]
     K = args.hidden or cfg.hidden
@@ -244,22 +402,22 @@ def main():
             def kstep():
                 gs.spmm(part.A, full_k, out=Y, mode=eff, task_nnz=args.task_nnz)
             kstep()
-        stream = torch.cuda.current_stream(dev)
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in range(args.steps)]
-        for a, b in evs:
-            a.record(stream)
-            kstep()
-            b.record(stream)
-        torch.cuda.synchronize(dev)
-        k_ms = float(np.mean([a.elapsed_time(b) for a, b in evs]))
+        k_ms = time_events(kstep, args.steps, dev)
         achieved = kbytes / (k_ms * 1e-3) / 1e9
         workload = f"{args.config}-{args.graph}-k{K}-{eff}"
         traffic, traffic_src = load_traffic(workload, B) if kbytes == B else (None, None)
         roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
                     "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "traffic": traffic, "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
-                    "kernel_ms": round(k_ms, 4), "algorithmic_bytes_per_launch": kbytes,
+                    "frac_vs_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
+                    "achieved_kind": "edge-centric algorithmic bytes (SURVEY.md §8d) / kernel "
+                                     "time; on the power-law graph hub rows are re-served from "
+                                     "the Infinity Cache, see variants.uniform for the "
+                                     "HBM-gather case",
+                    "traffic": traffic,
+                    "traffic_kind": "L2->fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE); "
+                                    "Infinity-Cache hits included (MI355X_MICROARCH.md:297)",
+                    "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
+                    "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": kbytes,
                     # compulsory bytes (every array touched once) beside the
                     # edge-centric count, so cache reuse on the gather is visible
                     "compulsory_bytes_per_launch": (
@@ -291,7 +449,10 @@ def main():
         t_comm = timed(lambda: part.all_gather(Zl), reps)
         t_sp = timed(lambda: gs.spmm(part.A, full, out=Y, mode=eff, task_nnz=args.task_nnz), reps)
         gathered = part.exchange_bytes_per_row(K)
-        dist_info = {"exchange": part.exchange, "halo_fraction": round(part.halo_fraction, 4),
+        import torch.distributed as dist
+        dist_info = {"world_size": dist.get_world_size() if world > 1 else 1,
+                     "backend": dist.get_backend() if world > 1 else None,
+                     "exchange": part.exchange, "halo_fraction": round(part.halo_fraction, 4),
                      "exchange_bytes_in_per_gpu": gathered,
                      "exchange_ms": round(t_comm, 4), "local_spmm_ms": round(t_sp, 4),
                      # the share of the pipelined step not covered by the
@@ -339,8 +500,17 @@ def main():
         rec["distributed"] = dist_info
     if alt:
         rec["alternatives"] = alt
+    if world == 1 and not args.partitioned and args.variants:
+        # SURVEY.md §8d second run: uniform degrees (no Infinity-Cache hub reuse)
+        del Z, Y
+        rec["variants"] = {"uniform": spmm_variant(cfg, "uniform", K, args.mode,
+                                                   max(args.steps, 5), dev)}
+    if world == 1 and not args.partitioned and args.train_step:
+        # BASELINE config 3: Twitter-US 2-layer fwd+bwd step (both layer-2 orders)
+        rec["train_step"] = train_step_bench(max(args.steps // 2, 5), max(args.warmup, 2), dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = cpu_baseline(H, K, args.cpu_budget)
+        rec["cpu_baseline"] = scipy_baseline(H, K)
+        rec["cpu_port"] = cpu_baseline(H, K, args.cpu_budget)
         try:
             rec["cpu_multicore"] = cpu_multicore(H, K, min(args.cpu_budget, 5.0))
         except Exception as exc:  # informational only

@@ -1,0 +1,62 @@
+"""bench.py's contract on the GPU: the N = 1 line, and the N > 1 row-partitioned path
+rehearsed with two ranks on the one MI355X over gloo (RCCL refuses two ranks on one device;
+the 8-GPU RCCL run is the driver's). Fresh child processes under torch.distributed.run, as
+the driver launches them."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.timeout(600)]
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _json_line(out: str) -> dict:
+    lines = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out[-2000:]
+    return json.loads(lines[0])
+
+
+def test_bench_single_gpu_line(cuda):
+    r = subprocess.run([sys.executable, "bench.py", "--config", "geotext", "--steps", "3",
+                        "--warmup", "1", "--no-train-step", "--no-cpu-baseline"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config",
+                "roofline", "variants"):
+        assert key in rec, key
+    assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
+    rf = rec["roofline"]
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["frac_vs_achievable"] > 0
+    assert rec["variants"]["uniform"]["kernel_ms"] > 0
+
+
+def test_bench_two_ranks_gloo(cuda):
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
+           "--gpus", "2", "--config", "twitter-us", "--steps", "3", "--warmup", "1",
+           "--dist-backend", "gloo"]
+    r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=500, env=env)
+    assert r.returncode == 0, r.stderr[-3000:]
+    rec = _json_line(r.stdout)
+    assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "row2"
+    d = rec["distributed"]
+    assert d["world_size"] == 2 and d["backend"] == "gloo"
+    for key in ("exchange", "exchange_ms", "local_spmm_ms", "comm_fraction"):
+        assert key in d, key
+    assert d["exchange_ms"] > 0 and d["local_spmm_ms"] > 0
+    assert "feature_parallel" in rec["alternatives"]

@@ -33,13 +33,15 @@ def _worker(rank, world, port, order, exchange, steps, q):
                                   device="cuda:0", W1=W1, W2=W2, order=order, exchange=exchange,
                                   regul_coefs=(1e-5, 1e-5))
         opt = model.make_optimizer()
-        hist = []
+        hist, grads0 = [], None
         for _ in range(steps):
             loss, acc = model.train_step(opt)
             hist.append((float(loss), float(acc)))
+            if grads0 is None:  # the all-reduced first-step gradients (Adam leaves p.grad)
+                grads0 = [p.grad.detach().cpu().numpy().copy() for p in model.params]
         torch.cuda.synchronize()
         params = [p.detach().cpu().numpy() for p in model.params]
-        q.put((rank, hist, params, model.part.exchange))
+        q.put((rank, hist, params, model.part.exchange, grads0))
     finally:
         dist.destroy_process_group()
 
@@ -65,12 +67,22 @@ def test_row_partitioned_training_matches_oracle(cuda, order, exchange):
     from oracle import gcn_oracle as O
     steps = 8
     ranks = _run(order, exchange, steps)
-    _, hist, params, used = ranks[0]
+    _, hist, params, used, grads0 = ranks[0]
     assert used == exchange
-    for _, h, ps, _ in ranks[1:]:  # replicas stay identical: one all-reduced gradient bucket
+    for _, h, ps, _, g0 in ranks[1:]:  # replicas stay identical: one all-reduced gradient bucket
         assert h == hist
         assert all(np.array_equal(a, b) for a, b in zip(ps, params))
+        assert all(np.array_equal(a, b) for a, b in zip(g0, grads0))
     H, X, Y, train, dev, test, init = problem(c=60)
+    # the partitioned backward (H^T = H, dist_train.py) against the float64 Theano-rule
+    # gradients at the initial parameters, before any Adam step amplifies rounding
+    W1, b1, W2, b2 = init
+    f0 = O.gcn_forward(X, H, W1, b1, W2, b2, train)
+    g64 = O.gcn_backward(X, H, W1, W2, f0, train, Y[train], regul_coefs=(1e-5, 1e-5))
+    for got, k in zip(grads0, ("W1", "b1", "W2", "b2")):
+        ref = g64[k]
+        err = np.abs(got - ref).max()
+        assert err < 1e-5 * max(1.0, np.abs(ref).max()), (k, err, np.abs(ref).max())
     ref, ref_params = O.mlpconv_train(X, H, Y, train, dev, *init, n_epochs=steps,
                                       regul_coefs=(1e-5, 1e-5), report_k_epoch=steps + 1)
     got = np.array([h[0] for h in hist])
