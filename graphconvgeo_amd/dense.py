@@ -268,6 +268,12 @@ class Projection:
         self.fwd = _WeightCache()
         self.bwd = _WeightCache()
 
+    def invalidate(self):
+        """Forget the cached copies: W changed without its version counter moving (a graph
+        replay's in-place Adam update)."""
+        self.fwd._key = None
+        self.bwd._key = None
+
     def matmul(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None
                ) -> torch.Tensor:
         return matmul(A, W, b)

@@ -286,6 +286,9 @@ class MLPCONV:
         def replay():
             opt.prepare()
             graph.replay()
+            # the replay's Adam update moved W2 in place without bumping its version counter:
+            # eager calls (validation, predict) must re-copy the padded weight
+            self._proj.invalidate()
             return static
 
         return replay

@@ -35,7 +35,7 @@ def test_layers_vs_golden(cuda, g):
     l1 = SparseConvolutionDenseLayer(F, H=H, num_units=K, W=g["W1"], b=g["b1"], device=cuda,
                                      mode="ordered")
     l2 = ConvolutionDenseLayer(l1, H=l1.H, num_units=C, W=g["W2"], b=g["b2"], device=cuda,
-                               mode="ordered")
+                               mode="ordered", nonlinearity="softmax")  # as mlpconv.py:214-217
     assert l2.H is l1.H  # one device copy of H shared, as mlpconv.py:214
     h = l1.get_output_for(X)
     assert np.array_equal(h.detach().cpu().numpy(), g["h32"])  # bitwise scipy fp32
@@ -107,3 +107,18 @@ def test_sparse_input_dense_layer(cuda):
     assert np.abs(lay.W.grad.cpu().numpy() - gW).max() < 1e-5 * np.abs(gW).max()  # fp32 sums of ~10^3 terms
     with pytest.raises(ValueError, match="must be sparse"):
         lay(torch.zeros((5, 800), device=cuda))
+
+
+def test_convolution_dense_layer_defaults_to_rectify(cuda, g):
+    """Lasagne DenseLayer's default nonlinearity is rectify; ConvolutionDenseLayer only adds H
+    (mlpconv.py:79-84), so without nonlinearity= its output is rectified, not a softmax."""
+    H, X = golden_inputs(g)
+    F, K = g["W1"].shape
+    C = g["W2"].shape[1]
+    l1 = SparseConvolutionDenseLayer(F, H=H, num_units=K, W=g["W1"], b=g["b1"], device=cuda,
+                                     mode="ordered")
+    l2 = ConvolutionDenseLayer(l1, H=l1.H, num_units=C, W=g["W2"], b=g["b2"], device=cuda,
+                               mode="ordered")
+    out = l2.get_output_for(l1.get_output_for(X), target_indices=g["idx"]).detach().cpu().numpy()
+    f = O.gcn_forward(X, H, g["W1"], g["b1"], g["W2"], g["b2"], g["idx"])
+    assert np.abs(out - O.relu(f["logits"])).max() < 1e-5
