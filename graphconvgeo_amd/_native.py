@@ -64,6 +64,8 @@ SIGNATURES = {
                                             _pi64, _p, _p]),
     "gcg_spgemm_products": (C.c_int, [_i64, _i64, _p, _p, _i64, _p, _pi64, _p]),
     "gcg_gemm_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, C.c_int, _p, _i64, _p]),
+    "gcg_gemm_nt_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, C.c_int, _p, _i64,
+                                  _p]),
     "gcg_project_softmax_xent_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p,
                                                C.c_float, _p, _p, _i64, _p, _p, _p]),
     "gcg_softmax_xent_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, C.c_float, _p, _p, _i64, _p,

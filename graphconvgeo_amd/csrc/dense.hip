@@ -378,6 +378,239 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
 #include "gemm_epilogue.inc"
 }
 
+// ---------------------------------------------------------------------------------------
+// gemm_nt_kernel<RT, G, WR, WC, S>: C = act(A . Bt^T + bias), both operands k-contiguous
+// (A: M x K row-major, Bt: N x K row-major -- the weight stored transposed, as
+// graphconvgeo_amd.dense keeps it), staged into LDS by the async LDS-DMA
+// (global_load_lds_dwordx4) through an S-deep ring of 32-deep k chunks.
+//
+//   * LDS image per stage: [BM + BN rows][32 floats], every row 128 B = 8 slots of 16 B,
+//     slot s of image row r stored at slot s ^ (r & 7): a fragment read (16 consecutive image
+//     rows x one slot per lane group) hits 16 distinct bank quads -- conflict-free
+//     ds_read_b128. The DMA writes LDS linearly (wave base + 16 B per lane), so the swizzle
+//     is applied to the per-lane GLOBAL source address (the involution s' <-> s ^ (r & 7)).
+//   * B image row order: within each 64-column group, row 16e + j holds column 4j + e, so
+//     the fragment of the strided MFMA tile e (columns 4j + e, j = 0..15) is 16 consecutive
+//     image rows, and a lane ends up with 4 ADJACENT output columns (acc[t][g][0..3]) ->
+//     dwordx4 stores; the same register layout as gemm_kernel (gemm_epilogue.inc).
+//   * A fragment: one ds_read_b128 per 16-row tile per 16-deep step gives the lane its 4
+//     k-values of the 4 v_mfma_f32_16x16x4_f32 substeps (k = k0 + 4q + e, permuted
+//     identically for A and B); B likewise, one ds_read_b128 per 16-column tile.
+//   * Sync: ONE raw s_barrier per chunk, after a counted `s_waitcnt vmcnt` that retires the
+//     chunk's own DMA (S = 2: vmcnt(0); S = 3: the next stage stays in flight). The barrier
+//     also fences the buffer the next DMA overwrites: every wave finished reading it (its
+//     MFMAs consumed the reads) before arriving. All LDS is one __shared__ array (a second
+//     object makes hipcc drain the DMA queue before every ds_read).
+//   * K tail: source addresses are clamped into the row; after the last chunk lands, its
+//     slots at k >= K are zeroed in LDS (one extra barrier per tile), so garbage in the
+//     operands' padding never meets a finite factor. Rows past M / columns past N read
+//     clamped rows and are never stored.
+//   * XCD-aware order (MI355X_MICROARCH.md: workgroup b runs on XCD b % 8): workgroup b takes
+//     logical tile remap(b), each XCD walking one contiguous range of tiles in row-block-major
+//     order, so the N / BN column tiles of a row block share one XCD's L2 copy of its A rows.
+// Numerics: exact f32 products, f32 accumulation in k order k0 + 4q + e inside each 16-deep
+// step (as gemm_kernel): equal to BLAS sgemm within f32 rounding.
+// ---------------------------------------------------------------------------------------
+typedef __attribute__((address_space(1))) const void* glds_src_t;
+typedef __attribute__((address_space(3))) void* glds_dst_t;
+
+__device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<glds_src_t>(reinterpret_cast<uintptr_t>(src)),
+                                   (glds_dst_t)(lds_wave_base), 16, 0, 0);
+}
+
+template <int RT, int G, int WR, int WC, int S>
+struct NtCfg {
+  static constexpr int NW = WR * WC;
+  static constexpr int NT = 64 * NW;
+  static constexpr int BM = 16 * RT * WR;
+  static constexpr int BN = 64 * G * WC;
+  static constexpr int KC = 32;
+  static constexpr int ROWS = BM + BN;            // image rows per stage
+  static constexpr int STAGE = ROWS * KC;         // floats per stage
+  static constexpr int NGLDS = ROWS / 8;          // DMA wave-instructions per stage
+  static constexpr int PER_WAVE = NGLDS / NW;     // (exact when S >= 3)
+  static constexpr int LDS_BYTES = S * STAGE * 4;
+  static constexpr int OCC = (2 * LDS_BYTES <= 160 * 1024) ? 2 : 1;
+  static_assert(ROWS % 8 == 0, "8 image rows per DMA instruction");
+  static_assert(S == 2 || NGLDS % NW == 0, "S >= 3 needs the same DMA count on every wave");
+  static_assert(S >= 2 && S <= 4, "2..4 stages");
+};
+
+template <int RT, int G, int WR, int WC, int S, int PF>
+__global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void gemm_nt_kernel(
+    int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ Bt,
+    int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
+    int n_col_tiles) {
+  using Cfg = NtCfg<RT, G, WR, WC, S>;
+  constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, KC = Cfg::KC, STAGE = Cfg::STAGE;
+  constexpr int EPI = 0;
+  __shared__ __attribute__((aligned(16))) float smem[S * STAGE];
+  float (*red)[WC][BM] = nullptr;  // (EPI = 1 only; gemm_epilogue.inc names it)
+  (void)red;
+
+  // XCD-aware bijective remap of the 1-D grid (cdna_hip_programming.md T1).
+  const int nwg = static_cast<int>(gridDim.x);
+  const int b = static_cast<int>(blockIdx.x);
+  const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+  const int row_tile = tile / n_col_tiles, col_tile = tile % n_col_tiles;
+  const int64_t row0 = static_cast<int64_t>(row_tile) * BM;
+  const int col0 = col_tile * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int j = lane & 15, q = lane >> 4;
+  const int colw = col0 + wc * G * 64;  // this wave's first output column (epilogue)
+
+  // ---- DMA source rows: this wave's instructions i = wave + NW * u cover image rows
+  // 8i .. 8i + 7; lane -> row 8i + lane / 8, LDS slot lane % 8, global slot (lane%8) ^ (row&7).
+  constexpr int NU = (Cfg::NGLDS + Cfg::NW - 1) / Cfg::NW;  // instructions per wave (max)
+  const float* src[NU];
+  int kofs[NU];  // 4 * global slot
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = wave + Cfg::NW * u;
+    const int r = 8 * i + (lane >> 3);
+    const int sl = (lane & 7) ^ (r & 7);
+    kofs[u] = 4 * sl;
+    if (r < BM) {
+      const int64_t gr = row0 + r;
+      src[u] = A + (gr < M ? gr : static_cast<int64_t>(M) - 1) * lda;
+    } else {
+      const int rb = r - BM;                       // B image row: group, tile e, lane j
+      const int n = col0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
+      src[u] = Bt + static_cast<int64_t>(n < N ? n : N - 1) * ldb;
+    }
+  }
+  const int kmax4 = (K - 1) & ~3;  // last 16-B segment holding a valid k
+  auto issue = [&](int chunk) {
+    float* stage = smem + (chunk % S) * STAGE;
+    const int kc0 = chunk * KC;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = wave + Cfg::NW * u;
+      if (NU * Cfg::NW != Cfg::NGLDS && i >= Cfg::NGLDS) break;  // wave-uniform
+      int k = kc0 + kofs[u];
+      k = k < kmax4 ? k : kmax4;
+      glds16(src[u] + k, stage + i * 256);  // instruction i fills 1 KB = image rows 8i..8i+7
+    }
+  };
+  auto lds_barrier = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f4 acc[RT][G][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  const int n_chunks = (K + KC - 1) / KC;
+  const int arow0 = wr * 16 * RT + j;       // A image row of tile 0 (lane j)
+  const int brow0 = BM + wc * G * 64 + j;   // B image row of group 0, tile e = 0 (lane j)
+  auto frag = [&](const float* stage, int row, int slot) -> f4 {
+    return *reinterpret_cast<const f4*>(stage + row * KC + 4 * (slot ^ (row & 7)));
+  };
+
+#pragma unroll
+  for (int c = 0; c < S - 1; ++c)
+    if (c < n_chunks) issue(c);
+  for (int c = 0; c < n_chunks; ++c) {
+    // retire this chunk's DMA (leave the later stages in flight), then one barrier
+    if constexpr (S == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (c + S - 2 < n_chunks) {
+        if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(Cfg::PER_WAVE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * Cfg::PER_WAVE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    lds_barrier();
+    const float* stage = smem + (c % S) * STAGE;
+    const int kc0 = c * KC;
+    if (kc0 + KC > K) {
+      // last chunk: zero the k >= K elements of every image row (both operands)
+      float* st = smem + (c % S) * STAGE;
+      for (int idx = tid; idx < Cfg::ROWS * KC; idx += NT) {
+        const int r = idx / KC, kk = idx % KC;
+        if (kc0 + kk >= K) {
+          const int sl = (kk >> 2) ^ (r & 7);
+          st[r * KC + 4 * sl + (kk & 3)] = 0.f;
+        }
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      lds_barrier();
+    }
+    if (c + S - 1 < n_chunks) issue(c + S - 1);
+    if constexpr (PF) {
+      // both 16-deep steps' fragments first: the second step's LDS reads are in flight
+      // during the first step's MFMAs (counted lgkmcnt waits)
+      const bool two = kc0 + 16 < K;  // wave-uniform; past K the LDS holds zeros anyway
+      f4 af[2][RT], bf[2][G][4];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) af[h][t] = frag(stage, arow0 + 16 * t, 4 * h + q);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            bf[h][g][e] = frag(stage, brow0 + 64 * g + 16 * e, 4 * h + q);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && !two) break;
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int t = 0; t < RT; ++t)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc[t][g][e] = mfma4(af[h][t][ss], bf[h][g][e][ss], acc[t][g][e]);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if (h == 1 && kc0 + 16 >= K) break;  // wave-uniform
+        f4 af[RT], bf[G][4];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) af[t] = frag(stage, arow0 + 16 * t, 4 * h + q);
+#pragma unroll
+        for (int g = 0; g < G; ++g)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) bf[g][e] = frag(stage, brow0 + 64 * g + 16 * e, 4 * h + q);
+#pragma unroll
+        for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+          for (int g = 0; g < G; ++g)
+#pragma unroll
+            for (int t = 0; t < RT; ++t)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                acc[t][g][e] = mfma4(af[t][ss], bf[g][e][ss], acc[t][g][e]);
+      }
+    }
+  }
+
+  const int32_t* labels = nullptr;
+  float scale = 0.f;
+  const float* scale_dev = nullptr;
+  float* loss_rows = nullptr;
+  float* correct_rows = nullptr;
+  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows;
+#include "gemm_epilogue.inc"
+}
+
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
 // exp, label logit and first-index argmax, then dlogits / probabilities. In-place safe.
 template <int NV>
@@ -755,9 +988,83 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
                         nullptr, 0.f, nullptr, nullptr, nullptr);
 }
 
+// NT GEMM tile variants: (RT, G, WR, WC, S). Default BM = 256 x BN = 64, two stages,
+// two workgroups per CU (80 KB of LDS each); the others are experiment knobs (GCG_NT_CFG).
+struct NtShape {
+  int RT, G, WR, WC, S, PF = 0;
+  int bm() const { return 16 * RT * WR; }
+  int bn() const { return 64 * G * WC; }
+};
+
+// Measured on one MI355X (tools/exp_gemm_nt.py, TFLOP/s, hipBLASLt in brackets):
+//   840k x 300 x 930  (2,1,4,1,2,PF) 110.9-111.5  (2,1,4,1,3) 107  (4,1,4,1,2) 108   [100-104]
+//   840k x 930 x 300  (2,1,4,1,3,PF) 113.6-114.4  (2,1,4,1,2) 109  (4,1,4,1,2) 111-112 [110-111]
+//   450k x 300 x 256  (2,1,4,1,2) 109  [119];  450k x 256 x 300  (2,1,4,1,2) 108.6  [87]
+// BM = 128 x BN = 64 with 48-72 KB of LDS runs 2-3 workgroups per CU: one workgroup's
+// barrier, DMA wait and epilogue overlap the others' MFMAs. A deeper ring pays off on the
+// longer K loop (K = 930).
+NtShape pick_nt_shape(int64_t K) {
+  NtShape sh = K > 512 ? NtShape{2, 1, 4, 1, 3, 1} : NtShape{2, 1, 4, 1, 2, 1};
+  if (const char* v = std::getenv("GCG_NT_CFG")) {
+    int a = 0, b = 0, c = 0, d = 0, e = 0, f = 0;
+    const int n = std::sscanf(v, "%d,%d,%d,%d,%d,%d", &a, &b, &c, &d, &e, &f);
+    if (n >= 5) sh = NtShape{a, b, c, d, e, n == 6 ? f : 0};
+  }
+  return sh;
+}
+
+gcg_status launch_nt(const NtShape& sh, hipStream_t st, int M, int N, int K, const float* A,
+                     int64_t lda, const float* Bt, int64_t ldb, const float* bias, int act,
+                     float* C, int64_t ldc) {
+  const int64_t rt = (M + sh.bm() - 1) / sh.bm(), ct = (N + sh.bn() - 1) / sh.bn();
+  if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: M too large");
+  const dim3 grid(static_cast<unsigned>(rt * ct));
+#define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                   \
+  if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_) {  \
+    hipLaunchKernelGGL((gemm_nt_kernel<rt_, g_, wr_, wc_, s_, pf_>), grid,                        \
+                       dim3(64 * (wr_) * (wc_)), 0, st, M, N, K, A, lda, Bt, ldb, bias, act, C,  \
+                       ldc, static_cast<int>(ct));                                               \
+    GCG_HIP_CHECK(hipGetLastError());                                                             \
+    return GCG_OK;                                                                                \
+  }
+  GCG_NT_CASE(2, 1, 4, 1, 2, 0)
+  GCG_NT_CASE(2, 1, 4, 1, 2, 1)
+  GCG_NT_CASE(2, 1, 4, 1, 3, 0)
+  GCG_NT_CASE(2, 1, 4, 1, 3, 1)
+  GCG_NT_CASE(1, 1, 4, 1, 2, 0)
+  GCG_NT_CASE(1, 1, 4, 1, 3, 0)
+  GCG_NT_CASE(3, 1, 4, 1, 2, 0)
+  GCG_NT_CASE(2, 2, 4, 1, 2, 0)
+  GCG_NT_CASE(2, 1, 2, 2, 2, 0)
+  GCG_NT_CASE(4, 1, 4, 1, 2, 0)
+#undef GCG_NT_CASE
+  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: no tile RT=%d G=%d WR=%d WC=%d S=%d", sh.RT,
+              sh.G, sh.WR, sh.WC, sh.S);
+}
+
 }  // namespace
 
 extern "C" {
+
+gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                           const float* Bt, int64_t ldbt, const float* bias, int act, float* C,
+                           int64_t ldc, gcg_stream_t stream) {
+  const char* fn = "gcg_gemm_nt_f32";
+  if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
+                static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
+  if (act != GCG_ACT_NONE && act != GCG_ACT_RELU)
+    return fail(GCG_ERR_INVALID_ARG, "%s: unknown act %d", fn, act);
+  gcg_status s;
+  // both operands are read as 16-B k-segments up to round4(K)
+  if ((s = check_dense(fn, A, lda, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
+  if ((s = check_dense(fn, Bt, ldbt, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
+  if ((s = check_dense(fn, C, ldc, N, true)) != GCG_OK) return s;
+  if (bias != nullptr && !aligned(bias, 4)) return fail(GCG_ERR_MISALIGNED, "%s: bias", fn);
+  if (M == 0) return GCG_OK;
+  return launch_nt(pick_nt_shape(K), static_cast<hipStream_t>(stream), int(M), int(N), int(K), A,
+                   lda, Bt, ldbt, bias, act, C, ldc);
+}
 
 gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         const float* B, int64_t ldb, const float* bias, int act, float* C,

@@ -8,7 +8,9 @@ Reference (Theano, host BLAS / CPU):
     predict_proba                          softmax rows                       mlpconv.py:329-335
 
 Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
-  matmul(A, W)                    C = A . W          gcg_gemm_f32 (grad A: g . W^T, same kernel)
+  matmul(A, W)                    C = A . W          gcg_gemm_nt_f32 on W^T (grad A: g . W^T,
+                                  the same kernel on W); grad W on gemm_tn
+  gemm(A, B) / gemm_nt(A, Bt)     the plain products (register-B / LDS-DMA kernels)
   project_softmax_xent(P, W, b, y)  loss, acc of softmax(P . W + b) against y, one fused
                                   kernel that never writes the logits; its gradient
                                   (softmax - onehot)/T is produced in the same pass
@@ -16,8 +18,8 @@ Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
   softmax(logits)                 predict_proba
   gemm_tn(A, B)                   C = A^T . B, the weight gradient h^T . g: a split-K MFMA kernel
                                   (reduction over ~10^6 rows), deterministic
-The plain forward / input-gradient GEMMs stay on hipBLASLt, measured faster on these shapes.
-There is no CPU path: CPU tensors raise.
+No product of the layer path goes to hipBLASLt / rocBLAS. There is no CPU path: CPU tensors
+raise.
 """
 from __future__ import annotations
 
@@ -112,6 +114,38 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
     actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
     with torch.cuda.device(A.device):
         call("gcg_gemm_f32", M, N, K, _ptr(A), _ld(A), _ptr(B), ldb, _ptr(bias), actc,
+             _ptr(out), _ld(out), _stream_handle(A.device))
+    return out
+
+
+def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = None,
+            act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """C = act(A . Bt^T + bias) on the LDS-DMA MFMA kernel (gcg_gemm_nt_f32): both operands
+    k-contiguous, 16-B aligned rows (A: M x K, Bt: N x K). The weight side is a transposed
+    padded copy (_WeightCache(transpose=True)) for A . W, or W itself (padded) for g . W^T."""
+    A = _aligned_operand(A, "A")
+    Bt = _aligned_operand(Bt, "Bt")
+    M, K = A.shape
+    N = Bt.shape[0]
+    if Bt.shape[1] != K:
+        raise ValueError(f"shape mismatch: A is {tuple(A.shape)}, Bt is {tuple(Bt.shape)}")
+    for t, n in ((A, "A"), (Bt, "Bt")):
+        if t.shape[0] > 1 and _ld(t) < (K + 3) // 4 * 4:
+            raise ValueError(f"{n} needs a row stride >= round4(K) (empty_dense)")
+    if bias is not None:
+        _require_cuda(bias, "bias")
+        if bias.numel() != N or bias.dtype != torch.float32:
+            raise ValueError(f"bias must be float32[{N}]")
+        bias = bias.detach().contiguous()
+    if out is None:
+        out = empty_dense(M, N, A.device)
+    elif out.shape != (M, N) or out.dtype != torch.float32 or (N > 1 and out.stride(1) != 1):
+        raise ValueError(f"out must be float32 [{M}, {N}] with unit column stride")
+    if M == 0:
+        return out
+    actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
+    with torch.cuda.device(A.device):
+        call("gcg_gemm_nt_f32", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt), _ptr(bias), actc,
              _ptr(out), _ld(out), _stream_handle(A.device))
     return out
 
@@ -224,17 +258,20 @@ def _placeholder_grad(W: torch.Tensor, like: torch.Tensor) -> torch.Tensor:
 
 
 class _MatMul(torch.autograd.Function):
-    """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88) and its gradients. Forward and dA = g . W^T
-    are plain GEMMs (hipBLASLt, measured faster on these shapes); the weight gradient
-    dW = A^T . g -- a reduction over ~10^6 rows into K x C -- runs on the split-K MFMA kernel
-    (gemm_tn, 1.13-1.28x hipBLASLt at Twitter-World shapes)."""
+    """C = A . W (+ b) (T.dot(h, W), mlpconv.py:88) and its gradients, every product on the
+    hand-written MFMA kernels: forward C = A . (W^T)^T and the input gradient
+    dA = g . W^T on the LDS-DMA NT GEMM (gemm_nt; W^T / W kept as padded copies in the
+    weight's Projection, re-copied when Adam moves W), the weight gradient dW = A^T . g -- a
+    reduction over ~10^6 rows into K x C -- on the split-K kernel (gemm_tn)."""
 
     @staticmethod
-    def forward(ctx, A, W, b, slot=None):
-        C = torch.matmul(A, W) if b is None else torch.addmm(b, A, W)
+    def forward(ctx, A, W, b, slot=None, proj=None):
+        proj = proj or Projection()
+        C = gemm_nt(A, proj.fwd.get(W, True), bias=b)
         ctx.save_for_backward(A, W)
         ctx.has_b = b is not None
         ctx.slot = slot
+        ctx.proj = proj
         return C
 
     @staticmethod
@@ -250,15 +287,25 @@ class _MatMul(torch.autograd.Function):
             else:
                 gW = gemm_tn(A, g)
         if ctx.needs_input_grad[0]:
-            gA = torch.matmul(g, W.t())
-        return gA, gW, gb, None
+            gA = gemm_nt(g, ctx.proj.bwd.get(W, False))  # g . W^T: Bt = W (padded K x round4(N))
+        return gA, gW, gb, None, None
+
+
+def projection_of(W: torch.Tensor) -> "Projection":
+    """The padded-copy cache of a weight, kept on the weight tensor itself (one per weight)."""
+    proj = getattr(W, "_gcg_projection", None)
+    if proj is None:
+        proj = Projection()
+        W._gcg_projection = proj
+    return proj
 
 
 def matmul(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Differentiable A . W (+ b); the weight gradient runs on the split-K MFMA kernel, on a
-    side stream so it overlaps the rest of the backward."""
+    """Differentiable A . W (+ b) on the MFMA kernels (forward and input gradient: gemm_nt;
+    weight gradient: gemm_tn on a side stream, overlapping the rest of the backward)."""
+    proj = projection_of(W)
     Wa, slot = _weight_on_side_stream(W)
-    return _MatMul.apply(A, Wa, b, slot)
+    return _MatMul.apply(A, Wa, b, slot, proj)
 
 
 class Projection:
@@ -276,7 +323,8 @@ class Projection:
 
     def matmul(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None
                ) -> torch.Tensor:
-        return matmul(A, W, b)
+        Wa, slot = _weight_on_side_stream(W)
+        return _MatMul.apply(A, Wa, b, slot, self)
 
     def softmax_xent(self, P, W, b, labels, denom: Optional[int] = None):
         if not torch.is_grad_enabled():  # evaluation: loss and hits only, no gradient buffer
@@ -374,8 +422,8 @@ class _ProjectXent(torch.autograd.Function):
             else:
                 gW = gemm_tn(P, G, scale=g)
         if ctx.needs_input_grad[0]:
-            # plain GEMM: hipBLASLt measured faster here (4.3 vs 5.2 ms at 840k x 930 x 300)
-            gP = torch.matmul(G, (W.detach() * g).t())
+            # dP = G . (g W)^T on the NT GEMM: Bt = g W, a scaled padded copy of W
+            gP = gemm_nt(G, ctx.proj.bwd.get(W, False, scale=g))
         return gP, gW, gb, None, None, None, None
 
 

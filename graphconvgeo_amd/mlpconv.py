@@ -287,8 +287,12 @@ class MLPCONV:
             opt.prepare()
             graph.replay()
             # the replay's Adam update moved W2 in place without bumping its version counter:
-            # eager calls (validation, predict) must re-copy the padded weight
+            # eager calls (validation, predict) must re-copy the padded weight copies
             self._proj.invalidate()
+            for p in self.params:
+                proj = getattr(p, "_gcg_projection", None)
+                if proj is not None:
+                    proj.invalidate()
             return static
 
         return replay

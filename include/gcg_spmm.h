@@ -287,6 +287,18 @@ gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t
                         float* C, int64_t ldc, gcg_stream_t stream);
 
 /*
+ * gcg_gemm_nt_f32: C = act(A . Bt^T + bias) with the second operand stored transposed
+ * (Bt: N x K row-major, ldbt >= round4(K), ldbt % 4 == 0, 16-B aligned base; A likewise with
+ * lda). The projection T.dot(h, W) (mlpconv.py:88) with Bt = W^T, and Theano's input
+ * gradient g . W^T with Bt = W itself. Both operands are k-contiguous, so both go to LDS
+ * through the asynchronous LDS-DMA (global_load_lds) in 32-deep chunks; the k tail is
+ * zeroed in LDS, so operand padding may hold anything. Same numerics as gcg_gemm_f32.
+ */
+gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                           const float* Bt, int64_t ldbt, const float* bias /*nullable*/,
+                           int act, float* C, int64_t ldc, gcg_stream_t stream);
+
+/*
  * Fused output layer + loss (N <= 1024; one workgroup owns whole rows):
  *   logits = A . W + bias                                       mlpconv.py:88-93
  *   labels != NULL: out = (softmax(logits) - onehot(labels)) * scale   (the logits gradient

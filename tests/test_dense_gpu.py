@@ -243,3 +243,64 @@ def test_lds_b_gemm_equals_register_b_gemm(cuda, M, K, N, monkeypatch):
         outs.append((dense.gemm(At, Bt), dense.gemm(At, Bt, bias=bt, act="relu")))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     _check_gemm(outs[0][1].cpu().numpy(), A, B, bias, relu=True)
+
+
+@pytest.mark.parametrize("M,K,N", [(1, 1, 1), (5, 3, 7), (33, 16, 64), (64, 17, 65),
+                                   (129, 31, 63), (257, 300, 256), (130, 300, 300),
+                                   (70, 300, 321), (96, 300, 930), (300, 930, 300),
+                                   (31, 65, 1024), (50, 40, 1500), (300, 129, 4),
+                                   (1000, 256, 300), (517, 33, 930)])
+def test_gemm_nt_vs_float64(cuda, M, K, N):
+    """gcg_gemm_nt_f32 (LDS-DMA staged, both operands k-contiguous): C = A . Bt^T."""
+    A, B = _rand((M, K), 11), _rand((K, N), 12)
+    Bt = _padded(B, cuda, transpose=True)  # N x round4(K)
+    C = dense.gemm_nt(torch.from_numpy(A).to(cuda), Bt).cpu().numpy()
+    _check_gemm(C, A, B)
+
+
+@pytest.mark.parametrize("cfg", ["2,1,4,1,2,0", "2,1,4,1,2,1", "2,1,4,1,3,0", "2,1,4,1,3,1",
+                                 "1,1,4,1,2,0", "1,1,4,1,3,0", "3,1,4,1,2,0", "2,2,4,1,2,0",
+                                 "2,1,2,2,2,0", "4,1,4,1,2,0"])
+def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
+    """Every instantiated tile (GCG_NT_CFG experiment knob) on ragged M / N / K, bias + relu."""
+    monkeypatch.setenv("GCG_NT_CFG", cfg)
+    M, K, N = 333, 301, 133
+    A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
+    C = dense.gemm_nt(torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True),
+                      bias=torch.from_numpy(b).to(cuda), act="relu").cpu().numpy()
+    _check_gemm(C, A, B, bias=b, relu=True)
+
+
+def test_gemm_nt_padding_never_leaks(cuda):
+    """The k tail is zeroed in LDS: NaN in the operands' padding columns (k >= K, inside
+    the row stride) and in rows past M / N must not reach C."""
+    M, K, N = 200, 298, 70
+    A, B = _rand((M, K), 16), _rand((K, N), 17)
+    Ap = torch.full((M, 300), float("nan"), device=cuda)
+    Ap[:, :K] = torch.from_numpy(A).to(cuda)
+    Btp = torch.full((N, 300), float("nan"), device=cuda)
+    Btp[:, :K] = torch.from_numpy(B.T.copy()).to(cuda)
+    C = dense.gemm_nt(Ap[:, :K], Btp[:, :K]).cpu().numpy()
+    assert np.isfinite(C).all()
+    _check_gemm(C, A, B)
+
+
+def test_matmul_autograd_on_nt_kernels(cuda):
+    """dense.matmul (T.dot(h, W) + b, mlpconv.py:88-93): forward, dA = g . W^T and dW, db."""
+    M, K, N = 700, 300, 129
+    A, W, b = _rand((M, K), 18), _rand((K, N), 19, 0.1), _rand((N,), 20)
+    G = _rand((M, N), 21)
+    At = torch.from_numpy(A).to(cuda).requires_grad_()
+    Wt = torch.nn.Parameter(torch.from_numpy(W).to(cuda))
+    bt = torch.nn.Parameter(torch.from_numpy(b).to(cuda))
+    C = dense.matmul(At, Wt, bt)
+    (C * torch.from_numpy(G).to(cuda)).sum().backward()
+    _check_gemm(C.detach().cpu().numpy(), A, W, bias=b)
+    _check_gemm(At.grad.cpu().numpy(), G, W.T.copy())
+    _check_gemm(Wt.grad.cpu().numpy(), A.T.copy(), G)
+    assert np.abs(bt.grad.cpu().numpy() - G.astype(np.float64).sum(0)).max() < 1e-4
+    # the weight moves in place (Adam): the cached transposed copy must follow
+    with torch.no_grad():
+        Wt.mul_(2.0)
+    C2 = dense.matmul(At.detach(), Wt, bt)
+    _check_gemm(C2.detach().cpu().numpy(), A, 2 * W, bias=b)
