@@ -379,20 +379,21 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
 }
 
 // ---------------------------------------------------------------------------------------
-// gemm_nt_kernel<RT, G, WR, WC, S>: C = act(A . Bt^T + bias), both operands k-contiguous
-// (A: M x K row-major, Bt: N x K row-major -- the weight stored transposed, as
+// gemm_nt_kernel<RT, G, WR, WC, S, PF, KC>: C = act(A . Bt^T + bias), both operands
+// k-contiguous (A: M x K row-major, Bt: N x K row-major -- the weight stored transposed, as
 // graphconvgeo_amd.dense keeps it), staged into LDS by the async LDS-DMA
-// (global_load_lds_dwordx4) through an S-deep ring of 32-deep k chunks.
+// (global_load_lds_dwordx4) through an S-deep ring of KC-deep k chunks (KC = 32 or 16).
 //
-//   * LDS image per stage: [BM + BN rows][32 floats], every row 128 B = 8 slots of 16 B,
-//     slot s of image row r stored at slot s ^ (r & 7): a fragment read (16 consecutive image
-//     rows x one slot per lane group) hits 16 distinct bank quads -- conflict-free
-//     ds_read_b128. The DMA writes LDS linearly (wave base + 16 B per lane), so the swizzle
-//     is applied to the per-lane GLOBAL source address (the involution s' <-> s ^ (r & 7)).
+//   * LDS image per stage: [BM + BN rows][KC floats], SL = KC/4 slots of 16 B per row, slot s
+//     of image row r stored at slot s ^ key(r): key = r & 7 for 8-slot rows, a permutation of
+//     (r >> 2) & 3 for 4-slot rows -- chosen so that each 16-lane group of a fragment read
+//     (16 consecutive image rows, slots q) hits 16 distinct bank quads: conflict-free
+//     ds_read_b128. The DMA writes LDS linearly (wave base + 16 B per lane), so the swizzle is
+//     applied to the per-lane GLOBAL source address (the involution s' <-> s ^ key(r)).
 //   * B image row order: within each 64-column group, row 16e + j holds column 4j + e, so
 //     the fragment of the strided MFMA tile e (columns 4j + e, j = 0..15) is 16 consecutive
 //     image rows, and a lane ends up with 4 ADJACENT output columns (acc[t][g][0..3]) ->
-//     dwordx4 stores; the same register layout as gemm_kernel (gemm_epilogue.inc).
+//     dwordx4 stores; the register layout of gemm_kernel (gemm_epilogue.inc).
 //   * A fragment: one ds_read_b128 per 16-row tile per 16-deep step gives the lane its 4
 //     k-values of the 4 v_mfma_f32_16x16x4_f32 substeps (k = k0 + 4q + e, permuted
 //     identically for A and B); B likewise, one ds_read_b128 per 16-column tile.
@@ -402,7 +403,7 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
 //     MFMAs consumed the reads) before arriving. All LDS is one __shared__ array (a second
 //     object makes hipcc drain the DMA queue before every ds_read).
 //   * K tail: source addresses are clamped into the row; after the last chunk lands, its
-//     slots at k >= K are zeroed in LDS (one extra barrier per tile), so garbage in the
+//     elements at k >= K are zeroed in LDS (one extra barrier per tile), so garbage in the
 //     operands' padding never meets a finite factor. Rows past M / columns past N read
 //     clamped rows and are never stored.
 //   * XCD-aware order (MI355X_MICROARCH.md: workgroup b runs on XCD b % 8): workgroup b takes
@@ -419,34 +420,53 @@ __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
                                    (glds_dst_t)(lds_wave_base), 16, 0, 0);
 }
 
-template <int RT, int G, int WR, int WC, int S>
+template <int RT, int G, int WR, int WC, int S, int KC>
 struct NtCfg {
   static constexpr int NW = WR * WC;
   static constexpr int NT = 64 * NW;
   static constexpr int BM = 16 * RT * WR;
   static constexpr int BN = 64 * G * WC;
-  static constexpr int KC = 32;
+  static constexpr int SL = KC / 4;               // 16-B slots per image row
+  static constexpr int RPI = 64 / SL;             // image rows per DMA instruction (1 KB)
   static constexpr int ROWS = BM + BN;            // image rows per stage
   static constexpr int STAGE = ROWS * KC;         // floats per stage
-  static constexpr int NGLDS = ROWS / 8;          // DMA wave-instructions per stage
+  static constexpr int NGLDS = ROWS / RPI;        // DMA wave-instructions per stage
   static constexpr int PER_WAVE = NGLDS / NW;     // (exact when S >= 3)
-  static constexpr int LDS_BYTES = S * STAGE * 4;
+  static constexpr int FLOATS = S * STAGE;
+  static constexpr int LDS_BYTES = FLOATS * 4;
   static constexpr int OCC = (2 * LDS_BYTES <= 160 * 1024) ? 2 : 1;
-  static_assert(ROWS % 8 == 0, "8 image rows per DMA instruction");
+  static_assert(KC == 16 || KC == 32, "4- or 8-slot image rows");
+  static_assert(ROWS % RPI == 0, "whole DMA instructions per stage");
   static_assert(S == 2 || NGLDS % NW == 0, "S >= 3 needs the same DMA count on every wave");
   static_assert(S >= 2 && S <= 4, "2..4 stages");
 };
 
-template <int RT, int G, int WR, int WC, int S, int PF>
-__global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void gemm_nt_kernel(
-    int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ Bt,
-    int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
-    int n_col_tiles) {
-  using Cfg = NtCfg<RT, G, WR, WC, S>;
-  constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, KC = Cfg::KC, STAGE = Cfg::STAGE;
-  constexpr int EPI = 0;
-  __shared__ __attribute__((aligned(16))) float smem[S * STAGE];
-  float (*red)[WC][BM] = nullptr;  // (EPI = 1 only; gemm_epilogue.inc names it)
+// Swizzle key of image row r (see above). 4-slot rows: pi((r >> 2) & 3), pi = {0, 2, 3, 1},
+// the permutation that makes every ds_read_b128 lane group {0-3,12-15,20-27}, ... of rows
+// j = 0..15 x slots q land on distinct bank quads.
+template <int SL>
+__device__ __forceinline__ int nt_key(int r) {
+  if constexpr (SL == 8) return r & 7;
+  else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;  // pi packed 2 bits each: 0, 2, 3, 1
+}
+
+template <int RT, int G, int WR, int WC, int S, int PF, int KC>
+__global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S, KC>::OCC)) void
+gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
+               const float* __restrict__ Bt, int64_t ldb, const float* __restrict__ bias, int act,
+               float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
+  using Cfg = NtCfg<RT, G, WR, WC, S, KC>;
+  constexpr int EPI = 0;  // plain epilogue only (gemm_epilogue.inc names the EPI = 1 operands)
+  const int32_t* labels = nullptr;
+  float scale = 0.f;
+  const float* scale_dev = nullptr;
+  float* loss_rows = nullptr;
+  float* correct_rows = nullptr;
+  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows;
+  constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, STAGE = Cfg::STAGE;
+  constexpr int SL = Cfg::SL, RPI = Cfg::RPI;
+  __shared__ __attribute__((aligned(16))) float smem[Cfg::FLOATS];
+  float (*red)[WC][BM] = nullptr;  // (EPI = 1 only)
   (void)red;
 
   // XCD-aware bijective remap of the 1-D grid (cdna_hip_programming.md T1).
@@ -466,15 +486,16 @@ __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void 
   const int colw = col0 + wc * G * 64;  // this wave's first output column (epilogue)
 
   // ---- DMA source rows: this wave's instructions i = wave + NW * u cover image rows
-  // 8i .. 8i + 7; lane -> row 8i + lane / 8, LDS slot lane % 8, global slot (lane%8) ^ (row&7).
+  // RPI*i .. RPI*i + RPI-1; lane -> row RPI*i + lane / SL, LDS slot lane % SL, global slot
+  // (lane % SL) ^ key(row).
   constexpr int NU = (Cfg::NGLDS + Cfg::NW - 1) / Cfg::NW;  // instructions per wave (max)
   const float* src[NU];
   int kofs[NU];  // 4 * global slot
 #pragma unroll
   for (int u = 0; u < NU; ++u) {
     const int i = wave + Cfg::NW * u;
-    const int r = 8 * i + (lane >> 3);
-    const int sl = (lane & 7) ^ (r & 7);
+    const int r = RPI * i + lane / SL;
+    const int sl = (lane % SL) ^ nt_key<SL>(r);
     kofs[u] = 4 * sl;
     if (r < BM) {
       const int64_t gr = row0 + r;
@@ -495,7 +516,7 @@ __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void 
       if (NU * Cfg::NW != Cfg::NGLDS && i >= Cfg::NGLDS) break;  // wave-uniform
       int k = kc0 + kofs[u];
       k = k < kmax4 ? k : kmax4;
-      glds16(src[u] + k, stage + i * 256);  // instruction i fills 1 KB = image rows 8i..8i+7
+      glds16(src[u] + k, stage + i * 256);  // instruction i fills 1 KB of the image
     }
   };
   auto lds_barrier = [&]() {
@@ -515,7 +536,25 @@ __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void 
   const int arow0 = wr * 16 * RT + j;       // A image row of tile 0 (lane j)
   const int brow0 = BM + wc * G * 64 + j;   // B image row of group 0, tile e = 0 (lane j)
   auto frag = [&](const float* stage, int row, int slot) -> f4 {
-    return *reinterpret_cast<const f4*>(stage + row * KC + 4 * (slot ^ (row & 7)));
+    return *reinterpret_cast<const f4*>(stage + row * KC + 4 * (slot ^ nt_key<SL>(row)));
+  };
+  auto mfma_step = [&](const f4 (&af)[RT], const f4 (&bf)[G][4]) {
+#pragma unroll
+    for (int ss = 0; ss < 4; ++ss)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) acc[t][g][e] = mfma4(af[t][ss], bf[g][e][ss], acc[t][g][e]);
+  };
+  auto read_step = [&](const float* stage, int h, f4 (&af)[RT], f4 (&bf)[G][4]) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) af[t] = frag(stage, arow0 + 16 * t, 4 * h + q);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bf[g][e] = frag(stage, brow0 + 64 * g + 16 * e, 4 * h + q);
   };
 
 #pragma unroll
@@ -541,73 +580,34 @@ __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S>::OCC)) void 
       float* st = smem + (c % S) * STAGE;
       for (int idx = tid; idx < Cfg::ROWS * KC; idx += NT) {
         const int r = idx / KC, kk = idx % KC;
-        if (kc0 + kk >= K) {
-          const int sl = (kk >> 2) ^ (r & 7);
-          st[r * KC + 4 * sl + (kk & 3)] = 0.f;
-        }
+        if (kc0 + kk >= K) st[r * KC + 4 * ((kk >> 2) ^ nt_key<SL>(r)) + (kk & 3)] = 0.f;
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       lds_barrier();
     }
     if (c + S - 1 < n_chunks) issue(c + S - 1);
-    if constexpr (PF) {
+    if constexpr (KC == 16) {
+      f4 af[RT], bf[G][4];
+      read_step(stage, 0, af, bf);
+      mfma_step(af, bf);
+    } else if constexpr (PF) {
       // both 16-deep steps' fragments first: the second step's LDS reads are in flight
-      // during the first step's MFMAs (counted lgkmcnt waits)
-      const bool two = kc0 + 16 < K;  // wave-uniform; past K the LDS holds zeros anyway
-      f4 af[2][RT], bf[2][G][4];
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-#pragma unroll
-        for (int t = 0; t < RT; ++t) af[h][t] = frag(stage, arow0 + 16 * t, 4 * h + q);
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int e = 0; e < 4; ++e)
-            bf[h][g][e] = frag(stage, brow0 + 64 * g + 16 * e, 4 * h + q);
-      }
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && !two) break;
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss)
-#pragma unroll
-          for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int t = 0; t < RT; ++t)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                acc[t][g][e] = mfma4(af[h][t][ss], bf[h][g][e][ss], acc[t][g][e]);
-      }
+      // during the first step's MFMAs (counted lgkmcnt waits); past K the LDS holds zeros
+      f4 af0[RT], bf0[G][4], af1[RT], bf1[G][4];
+      read_step(stage, 0, af0, bf0);
+      read_step(stage, 1, af1, bf1);
+      mfma_step(af0, bf0);
+      if (kc0 + 16 < K) mfma_step(af1, bf1);
     } else {
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        if (h == 1 && kc0 + 16 >= K) break;  // wave-uniform
-        f4 af[RT], bf[G][4];
-#pragma unroll
-        for (int t = 0; t < RT; ++t) af[t] = frag(stage, arow0 + 16 * t, 4 * h + q);
-#pragma unroll
-        for (int g = 0; g < G; ++g)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) bf[g][e] = frag(stage, brow0 + 64 * g + 16 * e, 4 * h + q);
-#pragma unroll
-        for (int ss = 0; ss < 4; ++ss)
-#pragma unroll
-          for (int g = 0; g < G; ++g)
-#pragma unroll
-            for (int t = 0; t < RT; ++t)
-#pragma unroll
-              for (int e = 0; e < 4; ++e)
-                acc[t][g][e] = mfma4(af[t][ss], bf[g][e][ss], acc[t][g][e]);
+      f4 af[RT], bf[G][4];
+      read_step(stage, 0, af, bf);
+      mfma_step(af, bf);
+      if (kc0 + 16 < K) {
+        read_step(stage, 1, af, bf);
+        mfma_step(af, bf);
       }
     }
   }
-
-  const int32_t* labels = nullptr;
-  float scale = 0.f;
-  const float* scale_dev = nullptr;
-  float* loss_rows = nullptr;
-  float* correct_rows = nullptr;
-  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows;
 #include "gemm_epilogue.inc"
 }
 
@@ -991,7 +991,7 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
 // NT GEMM tile variants: (RT, G, WR, WC, S). Default BM = 256 x BN = 64, two stages,
 // two workgroups per CU (80 KB of LDS each); the others are experiment knobs (GCG_NT_CFG).
 struct NtShape {
-  int RT, G, WR, WC, S, PF = 0;
+  int RT, G, WR, WC, S, PF = 0, KC = 32;
   int bm() const { return 16 * RT * WR; }
   int bn() const { return 64 * G * WC; }
 };
@@ -1006,27 +1006,43 @@ struct NtShape {
 NtShape pick_nt_shape(int64_t K) {
   NtShape sh = K > 512 ? NtShape{2, 1, 4, 1, 3, 1} : NtShape{2, 1, 4, 1, 2, 1};
   if (const char* v = std::getenv("GCG_NT_CFG")) {
-    int a = 0, b = 0, c = 0, d = 0, e = 0, f = 0;
-    const int n = std::sscanf(v, "%d,%d,%d,%d,%d,%d", &a, &b, &c, &d, &e, &f);
-    if (n >= 5) sh = NtShape{a, b, c, d, e, n == 6 ? f : 0};
+    int a = 0, b = 0, c = 0, d = 0, e = 0, f = 0, kc = 32;
+    const int n = std::sscanf(v, "%d,%d,%d,%d,%d,%d,%d", &a, &b, &c, &d, &e, &f, &kc);
+    if (n >= 5) sh = NtShape{a, b, c, d, e, n >= 6 ? f : 0, n == 7 ? kc : 32};
   }
   return sh;
 }
 
-gcg_status launch_nt(const NtShape& sh, hipStream_t st, int M, int N, int K, const float* A,
-                     int64_t lda, const float* Bt, int64_t ldb, const float* bias, int act,
-                     float* C, int64_t ldc) {
-  const int64_t rt = (M + sh.bm() - 1) / sh.bm(), ct = (N + sh.bn() - 1) / sh.bn();
-  if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: M too large");
-  const dim3 grid(static_cast<unsigned>(rt * ct));
-#define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                   \
-  if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_) {  \
-    hipLaunchKernelGGL((gemm_nt_kernel<rt_, g_, wr_, wc_, s_, pf_>), grid,                        \
-                       dim3(64 * (wr_) * (wc_)), 0, st, M, N, K, A, lda, Bt, ldb, bias, act, C,  \
-                       ldc, static_cast<int>(ct));                                               \
-    GCG_HIP_CHECK(hipGetLastError());                                                             \
-    return GCG_OK;                                                                                \
-  }
+struct NtArgs {
+  int M, N, K;
+  const float* A;
+  int64_t lda;
+  const float* Bt;
+  int64_t ldb;
+  const float* bias;
+  int act;
+  float* C;
+  int64_t ldc;
+};
+
+template <int RT, int G, int WR, int WC, int S, int PF, int KC>
+gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
+  constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
+  const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
+  if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
+  hipLaunchKernelGGL((gemm_nt_kernel<RT, G, WR, WC, S, PF, KC>),
+                     dim3(static_cast<unsigned>(rt * ct)), dim3(64 * WR * WC), 0, st, a.M, a.N,
+                     a.K, a.A, a.lda, a.Bt, a.ldb, a.bias, a.act, a.C, a.ldc,
+                     static_cast<int>(ct));
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
+#define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                  \
+  if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_ && \
+      sh.KC == 32)                                                                               \
+    return launch_nt_t<rt_, g_, wr_, wc_, s_, pf_, 32>(a, st);
   GCG_NT_CASE(2, 1, 4, 1, 2, 0)
   GCG_NT_CASE(2, 1, 4, 1, 2, 1)
   GCG_NT_CASE(2, 1, 4, 1, 3, 0)
@@ -1038,8 +1054,10 @@ gcg_status launch_nt(const NtShape& sh, hipStream_t st, int M, int N, int K, con
   GCG_NT_CASE(2, 1, 2, 2, 2, 0)
   GCG_NT_CASE(4, 1, 4, 1, 2, 0)
 #undef GCG_NT_CASE
-  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: no tile RT=%d G=%d WR=%d WC=%d S=%d", sh.RT,
-              sh.G, sh.WR, sh.WC, sh.S);
+  if (sh.KC == 16 && sh.RT == 2 && sh.G == 1 && sh.WR == 4 && sh.WC == 1 && sh.S == 3)
+    return launch_nt_t<2, 1, 4, 1, 3, 0, 16>(a, st);
+  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: no tile RT=%d G=%d WR=%d WC=%d S=%d PF=%d KC=%d",
+              sh.RT, sh.G, sh.WR, sh.WC, sh.S, sh.PF, sh.KC);
 }
 
 }  // namespace
@@ -1062,8 +1080,8 @@ gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
   if ((s = check_dense(fn, C, ldc, N, true)) != GCG_OK) return s;
   if (bias != nullptr && !aligned(bias, 4)) return fail(GCG_ERR_MISALIGNED, "%s: bias", fn);
   if (M == 0) return GCG_OK;
-  return launch_nt(pick_nt_shape(K), static_cast<hipStream_t>(stream), int(M), int(N), int(K), A,
-                   lda, Bt, ldbt, bias, act, C, ldc);
+  NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
+  return launch_nt(pick_nt_shape(K), static_cast<hipStream_t>(stream), a);
 }
 
 gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,

@@ -66,6 +66,22 @@ __device__ __forceinline__ Vec<VEC> load_vec(const float* __restrict__ p) {
   return r;
 }
 
+// Non-temporal (streaming) store: Y is written once and not re-read by this kernel, so it
+// need not displace the gathered operand's hot rows from the caches (experiment knob
+// GCG_SPMM_NT_STORE=1).
+template <int VEC>
+__device__ __forceinline__ void store_vec_nt(float* __restrict__ p, const Vec<VEC>& v) {
+  if constexpr (VEC == 4) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{v.x[0], v.x[1], v.x[2], v.x[3]}, reinterpret_cast<f4v*>(p));
+  } else if constexpr (VEC == 2) {
+    typedef float f2v __attribute__((ext_vector_type(2)));
+    __builtin_nontemporal_store(f2v{v.x[0], v.x[1]}, reinterpret_cast<f2v*>(p));
+  } else {
+    __builtin_nontemporal_store(v.x[0], p);
+  }
+}
+
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* __restrict__ p, const Vec<VEC>& v) {
   if constexpr (VEC == 4) {
@@ -174,7 +190,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
     float* __restrict__ ws, int64_t ldws, int xcd_remap, uint8_t* __restrict__ gate,
-    int64_t ldgate) {
+    int64_t ldgate, int nt_store) {
   // Optional XCD-aware mapping (experiment): blocks b and b + 8 share an XCD under the
   // observed round-robin dispatch, so block b takes task block (b % 8) * ceil(nb / 8) + b / 8
   // and each XCD walks one contiguous range of rows. Placement is speed-only, never correctness.
@@ -241,7 +257,10 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
       if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], acc[k]);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = apply_act(acc[k].x[q], act);
-      store_vec<VEC>(yrow + col[k], acc[k]);
+      if (nt_store)
+        store_vec_nt<VEC>(yrow + col[k], acc[k]);
+      else
+        store_vec<VEC>(yrow + col[k], acc[k]);
     }
   }
 }
@@ -297,9 +316,10 @@ template <int VEC, int NCH, int U, int WPB>
 void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   const dim3 grid((a.n_tasks + WPB - 1) / WPB, n_panels);
   static const int xcd = env_int("GCG_XCD_REMAP");
+  const int nts = env_int("GCG_SPMM_NT_STORE");
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
-                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate, a.ldgate);
+                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate, a.ldgate, nts);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)

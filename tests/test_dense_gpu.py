@@ -260,7 +260,7 @@ def test_gemm_nt_vs_float64(cuda, M, K, N):
 
 @pytest.mark.parametrize("cfg", ["2,1,4,1,2,0", "2,1,4,1,2,1", "2,1,4,1,3,0", "2,1,4,1,3,1",
                                  "1,1,4,1,2,0", "1,1,4,1,3,0", "3,1,4,1,2,0", "2,2,4,1,2,0",
-                                 "2,1,2,2,2,0", "4,1,4,1,2,0"])
+                                 "2,1,2,2,2,0", "4,1,4,1,2,0", "2,1,4,1,3,0,16"])
 def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
     """Every instantiated tile (GCG_NT_CFG experiment knob) on ragged M / N / K, bias + relu."""
     monkeypatch.setenv("GCG_NT_CFG", cfg)

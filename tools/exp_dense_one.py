@@ -1,6 +1,7 @@
 #!/usr/bin/env python
-"""Profiling driver: 3 launches each of the fused output kernel (default tile) and the plain
-MFMA GEMM at Twitter-World's 840k x 300 x 930 (for rocprofv3 --pmc passes)."""
+"""Profiling driver: 3 launches each of the fused output kernel (default tile), the plain
+register-B MFMA GEMM and the LDS-DMA NT GEMM (forward 840k x 300 x 930, input gradient
+840k x 930 x 300) at Twitter-World's output-layer shapes (for rocprofv3 --pmc passes)."""
 import os
 import sys
 
@@ -24,5 +25,11 @@ for _ in range(3):
     dense._fused(P, Wp, b, y, 1.0 / T, None, G, loss, hits)
 for _ in range(3):
     dense.gemm(P, Wp, bias=b, out=G)
+Wt = dense._WeightCache().get(W, True)
+for _ in range(3):
+    dense.gemm_nt(P, Wt, bias=b, out=G)
+dP = empty_dense(T, K, dev)
+for _ in range(3):
+    dense.gemm_nt(G, Wp, out=dP)
 torch.cuda.synchronize()
 print("done")
