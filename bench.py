@@ -485,10 +485,10 @@ def main():
     value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
-        "value": round(value, 1), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
-        "warmup": args.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+        "value": round(value), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
-        "edges_per_s": round(nnz / (ms * 1e-3), 1),
+        "edges_per_s": round(nnz / (ms * 1e-3)),
         "config": {"workload": f"{cfg.name} H.Z SpMM fwd, {args.graph} degrees", "nodes": N,
                    "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": f"{args.mode}->{eff}",
                    "parallelism": f"row{world}" if world > 1 else "single",
