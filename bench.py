@@ -232,10 +232,13 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
            "F": cfg.n_features, "K": K, "C": C, "train_rows": int(train.size),
            "data": "synthetic", "data_gen_s": round(t_gen, 1), "steps": steps, "warmup": warmup}
     clf = None
-    for order in ("reference", "propagate_first"):
-        clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, order=order)
+    for order, graph in (("reference", False), ("propagate_first", False),
+                         ("propagate_first", True)):
+        clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, order=order,
+                      use_graph=graph)
         clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H and X
         y_train = torch.as_tensor(Y[train].astype(np.int32), device=dev)
+        clf.n_epochs = 1  # lets _make_train_step capture the epoch when use_graph
         step = clf._make_train_step(LasagneAdam(clf.params), y_train)
         for _ in range(warmup):
             step()
@@ -245,7 +248,8 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
             loss, _acc = step()
         torch.cuda.synchronize(dev)
         ms = (time.perf_counter() - t1) / max(steps, 1) * 1e3
-        out[order] = {"ms_per_step": round(ms, 3), "loss": round(float(loss), 5)}
+        out[order + ("_hip_graph" if graph else "")] = {"ms_per_step": round(ms, 3),
+                                                          "loss": round(float(loss), 5)}
     # each SpMM of the step alone, on the last model's device operands
     A, Xd = clf.l_hid1.H, clf.Xd
     rows = clf.rows["train"]

@@ -49,6 +49,8 @@ SIGNATURES = {
                                              C.c_size_t, _p]),
     "gcg_spmm_plan_host": (C.c_int, [_i64, _p, _p, _i64, _i64, C.c_int, _p, _i64, _pi64, _p,
                                      _i64, _pi64, _pi64]),
+    "gcg_adam_step_f32": (C.c_int, [_i64, _p, _p, _p, _p, _p, C.c_float, C.c_float, C.c_float,
+                                    _p]),
     "gcg_csr_validate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p]),
     "gcg_index_csr": (C.c_int, [_i64, _p, _i64, _p, _p, _p, C.c_size_t, _psz, _p]),
     "gcg_scatter_add_rows_f32": (C.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p]),

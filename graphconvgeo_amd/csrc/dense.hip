@@ -785,29 +785,53 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
       }
 }
 
-// C[m][n] = scale * sum_{s in order} part[s][m][n]; one thread per (m, 4 columns).
-__global__ __launch_bounds__(256) void gemm_tn_reduce_kernel(
+// C[m][n] = scale * sum over the S split partials part[s][m][n], deterministic. One workgroup
+// per (row m, 64 column quads): wave w of the 8 sums the splits s = w, w + 8, ... (4 loads in
+// flight per lane), then the 8 wave sums are added in wave order through LDS. (One thread per
+// output quad summing all S serially left ~1 wave per CU in flight: 0.57 ms for Twitter-US.)
+constexpr int kTnRedWaves = 8;
+__global__ __launch_bounds__(64 * kTnRedWaves) void gemm_tn_reduce_kernel(
     int M, int N, int S, const float* __restrict__ part, int Mp, int Np,
     const float* __restrict__ scale_dev, float* __restrict__ C, int64_t ldc, int vec) {
-  const int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+  __shared__ f4 red[kTnRedWaves][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int nq = (N + 3) / 4;
-  if (i >= static_cast<int64_t>(M) * nq) return;
-  const int m = static_cast<int>(i / nq), n = static_cast<int>(i % nq) * 4;
-  const float* src = part + static_cast<int64_t>(m) * Np + n;
-  f4 acc = *reinterpret_cast<const f4*>(src);
-  for (int s = 1; s < S; ++s) {
-    const f4 v = *reinterpret_cast<const f4*>(src + static_cast<int64_t>(s) * Mp * Np);
-    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  for (int m = blockIdx.y; m < M; m += gridDim.y) {  // grid.y <= 65535
+  if (m != static_cast<int>(blockIdx.y)) __syncthreads();  // red is reused
+  const int qd = static_cast<int>(blockIdx.x) * 64 + lane;  // column quad
+  const int qc = qd < nq ? qd : nq - 1;
+  const float* src = part + static_cast<int64_t>(m) * Np + 4 * qc;
+  const int64_t stride = static_cast<int64_t>(Mp) * Np;
+  f4 acc = {0.f, 0.f, 0.f, 0.f};
+  int s = w;
+  for (; s + 3 * kTnRedWaves < S; s += 4 * kTnRedWaves) {
+    const f4 v0 = *reinterpret_cast<const f4*>(src + s * stride);
+    const f4 v1 = *reinterpret_cast<const f4*>(src + (s + kTnRedWaves) * stride);
+    const f4 v2 = *reinterpret_cast<const f4*>(src + (s + 2 * kTnRedWaves) * stride);
+    const f4 v3 = *reinterpret_cast<const f4*>(src + (s + 3 * kTnRedWaves) * stride);
+    acc += v0;
+    acc += v1;
+    acc += v2;
+    acc += v3;
   }
+  for (; s < S; s += kTnRedWaves) acc += *reinterpret_cast<const f4*>(src + s * stride);
+  red[w][lane] = acc;
+  __syncthreads();
+  if (w != 0 || qd >= nq) continue;
+  f4 t = red[0][lane];
+#pragma unroll
+  for (int i = 1; i < kTnRedWaves; ++i) t += red[i][lane];
   const float sc = scale_dev ? *scale_dev : 1.0f;
+  const int n = 4 * qd;
   float* crow = C + static_cast<int64_t>(m) * ldc;
-  const f4 o = {acc.x * sc, acc.y * sc, acc.z * sc, acc.w * sc};
+  const f4 o = {t.x * sc, t.y * sc, t.z * sc, t.w * sc};
   if (vec && n + 3 < N) {
     *reinterpret_cast<f4*>(crow + n) = o;
   } else {
 #pragma unroll
     for (int e = 0; e < 4; ++e)
       if (n + e < N) crow[n + e] = o[e];
+  }
   }
 }
 
@@ -1191,11 +1215,11 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
 #undef GCG_TN_CASE
   GCG_HIP_CHECK(hipGetLastError());
-  const int64_t threads = M * ((N + 3) / 4);
   const int vec = (ldc % 4 == 0 && aligned(C, 16)) ? 1 : 0;
-  hipLaunchKernelGGL(gemm_tn_reduce_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)),
-                     dim3(256), 0, s, int(M), int(N), p.S, part, p.Mp, p.Np, scale_dev, C, ldc,
-                     vec);
+  const dim3 rgrid(static_cast<unsigned>(((N + 3) / 4 + 63) / 64),
+                   static_cast<unsigned>(std::min<int64_t>(M, 65535)));
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, rgrid, dim3(64 * kTnRedWaves), 0, s, int(M), int(N),
+                     p.S, part, p.Mp, p.Np, scale_dev, C, ldc, vec);
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }

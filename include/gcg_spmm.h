@@ -203,6 +203,16 @@ gcg_status gcg_column_sum_f32(int64_t M, int64_t K, const float* X, int64_t ldx,
                               void* workspace, size_t workspace_bytes, gcg_stream_t stream);
 
 /*
+ * lasagne.updates.adam (mlpconv.py:263) for one float32 parameter of n elements, in place:
+ *   m = b1*m + (1-b1)*g;  v = b2*v + (1-b2)*g*g;  p -= a_t*m / (sqrt(v) + eps),
+ * with a_t = lr*sqrt(1-b2^t)/(1-b1^t) read from the device scalar *step_dev (so the call can
+ * sit inside a captured HIP graph and be replayed with a new step size).
+ */
+gcg_status gcg_adam_step_f32(int64_t n, float* p, const float* g, float* m, float* v,
+                             const float* step_dev, float beta1, float beta2, float eps,
+                             gcg_stream_t stream);
+
+/*
  * CSR transpose on the device (CSR(X^T) for the X^T . dZ1 gradient of
  * mlpconv.py:71). Output is sorted by (row, col) with stable order for equal
  * entries. out_indptr int32[n_cols+1], out_indices int32[nnz], out_vals f32[nnz].

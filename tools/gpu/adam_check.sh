@@ -1,0 +1,7 @@
+#!/bin/bash
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/adam
+mkdir -p $out
+timeout -k 10 300 python -u -m pytest -x -q --tb=short --timeout 300 --timeout-method thread -m gpu tests/test_mlpconv_gpu.py -k "adam" > $out/tests.log 2>&1 || { grep -E 'Error|assert|FAILED|passed|failed' $out/tests.log | cut -c1-300 | tail -30; exit 1; }
+tail -1 $out/tests.log
