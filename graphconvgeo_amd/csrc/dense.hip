@@ -68,7 +68,7 @@ constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 
 
 template <int RT, int G, int WR, int WC, int EPI, int PF>
-__global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void gemm_kernel(
+__global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) void gemm_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
@@ -150,14 +150,18 @@ __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void ge
   };
 
   // ---- B fragments for one 16-deep k-step: bf[g][e] = B[k0 + 4q + e][bcol[g] .. +3] ----
-  auto load_b = [&](f4 (&bf)[G][4], int k0) {
+  // Fragments (g, e) with unit u = 4g + e in [u0, u1) only (the split ping-pong body loads
+  // one part of the set at a time).
+  auto load_b = [&](f4 (&bf)[G][4], int k0, int u0 = 0, int u1 = 4 * G) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       int k = k0 + 4 * q + e;
       k = k < K ? k : K - 1;  // A is zero there; any finite B row does
       const float* brow = B + static_cast<int64_t>(k) * ldb;
 #pragma unroll
-      for (int g = 0; g < G; ++g) bf[g][e] = *reinterpret_cast<const f4*>(brow + bcol[g]);
+      for (int g = 0; g < G; ++g)
+        if (4 * g + e >= u0 && 4 * g + e < u1)
+          bf[g][e] = *reinterpret_cast<const f4*>(brow + bcol[g]);
     }
   };
 
@@ -167,7 +171,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void ge
   // AGPR copies and spills -- and slower with the single-buffer body.
   constexpr bool SKIP = PF != 0;
   const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
-  auto compute = [&](const f4 (&bf)[G][4], int buf, int s) {
+  auto compute = [&](const f4 (&bf)[G][4], int buf, int s, int u0 = 0, int u1 = 4 * G) {
     f4 af[RT];
 #pragma unroll
     for (int t = 0; t < RT; ++t)
@@ -176,6 +180,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void ge
     for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int g = 0; g < G; ++g) {
+        if (4 * g + e < u0 || 4 * g + e >= u1) continue;  // compile-time after unrolling
         if (SKIP && g >= ngv) continue;  // scalar branch: group entirely past N
 #pragma unroll
         for (int t = 0; t < RT; ++t) {
@@ -197,7 +202,31 @@ __global__ __launch_bounds__(64 * WR * WC, (PF && WR * WC == 4) ? 1 : 2) void ge
   store_a(0);
   lds_barrier();
   f4 b0[G][4];
-  if constexpr (PF) {
+  if constexpr (PF >= 2) {
+    // Split ping-pong in one register set: b0's 4G fragments (g, e) are cut into NP = PF
+    // parts that rotate, each part loaded for the next 16-deep step as soon as its MFMAs for
+    // this step are issued, so a wave computes the other parts while a part's loads are in
+    // flight (PF = 1's latency hiding at PF = 0's register count, which keeps 2 workgroups
+    // per CU). Every accumulator still sees e = 0..3 in order: bitwise equal to PF = 0.
+    constexpr int NP = PF, NU = 4 * G;
+    static_assert(NU % NP == 0, "parts split the fragments evenly");
+#pragma unroll
+    for (int p = 0; p < NP; ++p) load_b(b0, 0, p * NU / NP, (p + 1) * NU / NP);
+    for (int c = 0; c < n_chunks; ++c) {
+      const int buf = c & 1;
+      const int k0 = c * KC;
+      load_a(k0 + KC);  // past K: clamped and zeroed, never used
+#pragma unroll
+      for (int st = 0; st < 2; ++st)  // k0 + 16 >= K: A is zero there
+#pragma unroll
+        for (int p = 0; p < NP; ++p) {
+          compute(b0, buf, st, p * NU / NP, (p + 1) * NU / NP);
+          load_b(b0, k0 + 16 * (st + 1), p * NU / NP, (p + 1) * NU / NP);
+        }
+      store_a(buf ^ 1);
+      lds_barrier();
+    }
+  } else if constexpr (PF) {
     f4 b1[G][4];
     load_b(b0, 0);
     for (int c = 0; c < n_chunks; ++c) {
@@ -920,6 +949,14 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
   GCG_GEMM_CASE(2, 2, 1, 4, 0)
   GCG_GEMM_CASE(2, 3, 1, 4, 0)
   GCG_GEMM_CASE(2, 4, 2, 4, 0)
+  GCG_GEMM_CASE(2, 4, 1, 4, 2)
+  GCG_GEMM_CASE(2, 3, 1, 4, 2)
+  GCG_GEMM_CASE(2, 2, 1, 4, 2)
+  GCG_GEMM_CASE(2, 4, 1, 4, 4)
+  GCG_GEMM_CASE(2, 4, 1, 4, 8)
+  GCG_GEMM_CASE(2, 4, 1, 4, 16)
+  GCG_GEMM_CASE(2, 3, 1, 4, 4)
+  GCG_GEMM_CASE(2, 2, 1, 4, 4)
   GCG_GEMM_CASE(2, 1, 4, 1, 1)
   GCG_GEMM_CASE(2, 2, 4, 1, 1)
   GCG_GEMM_CASE(2, 3, 4, 1, 1)
@@ -938,10 +975,14 @@ Shape pick_shape(int64_t N, bool fused) {
   // Wide (WC = 4) tiles, measured on Twitter-World's 840k x 300 x 930 (TFLOP/s, plain / fused):
   //   RT = 4, B ping-pong, 1 workgroup per CU          92.8 / 78.7   <- plain default
   //   RT = 2, B ping-pong, 1 workgroup per CU          83.0 / 72.2
-  //   RT = 2, one B set, 2 workgroups per CU           91.8 / 85.0   <- fused default: the
-  //       second workgroup hides B latency and overlaps the other's softmax epilogue + stores
+  //   RT = 2, one B set, 2 workgroups per CU           91.8 / 85.0-87.4: the second
+  //       workgroup hides B latency and overlaps the other's softmax epilogue + stores
+  //   ... + B set split into 2 / 4 / 8 / 16 rotating parts, groups past N skipped
+  //                                                    - / 92.3, 96.4, 96.8, 95.4
+  //                                                    <- fused default: 8 parts (PF = 8)
   //   RT = 2, one B set, 8-wave workgroup              93.1 / 83.8
-  // Knobs for experiments: GCG_GEMM_RT=2, GCG_GEMM_8W=1, GCG_GEMM_OCC2=0/1.
+  // Knobs for experiments: GCG_GEMM_RT=2, GCG_GEMM_8W=1, GCG_GEMM_OCC2=0/1,
+  // GCG_GEMM_SPLIT=0/2/4/8/16 (B parts of the 2-workgroup tiles).
   const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
   // Plain products: B through LDS (gemm_bl_kernel), measured on the train step's shapes
   // (tools/exp_gemm_bl.py, TFLOP/s, B-from-L2 gemm_kernel -> LDS-B):
@@ -961,7 +1002,12 @@ Shape pick_shape(int64_t N, bool fused) {
     if (env_int("GCG_GEMM_8W") && g == 4) return Shape{2, 4, 2, 4, 0};
     const char* occ = std::getenv("GCG_GEMM_OCC2");
     const bool occ2 = occ ? std::atoi(occ) != 0 : fused;
-    if (occ2 && g >= 2) return Shape{2, g, 1, 4, 0};
+    if (occ2 && g >= 2) {
+      const char* spv = std::getenv("GCG_GEMM_SPLIT");  // B ping-pong parts (0: none)
+      const int sp = spv ? std::atoi(spv) : 8;
+      const int np = sp >= 8 && g == 4 ? (sp >= 16 ? 16 : 8) : sp >= 4 ? 4 : sp >= 2 ? 2 : 0;
+      return Shape{2, g, 1, 4, np};
+    }
     return Shape{g >= 2 ? rt : 2, std::max(g, 1), 1, 4};
   }
   return Shape{2, std::max(groups, 1), 4, 1};

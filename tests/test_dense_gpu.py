@@ -115,6 +115,27 @@ def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
     assert torch.equal(loss, loss2)
 
 
+@pytest.mark.parametrize("M,K,N", [(37, 16, 129), (300, 300, 256), (513, 300, 930), (70, 33, 1024)])
+def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
+    """The B ping-pong split (GCG_GEMM_SPLIT = 0 / 2 / 4 / 8 / 16 register-set parts) only reorders
+    MFMAs between distinct accumulators: gradient, loss and hits are bitwise equal."""
+    P, W, b = _rand((M, K), 21, 0.3), _rand((K, N), 22, 0.3), _rand((N,), 23)
+    y = np.random.default_rng(24).integers(0, N, M).astype(np.int32)
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    Wp = dense.Projection().fwd.get(Wt, False)
+    outs = []
+    for split in ("0", "2", "4", "8", "16"):
+        monkeypatch.setenv("GCG_GEMM_SPLIT", split)
+        G = empty_dense(M, N, cuda)
+        loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
+        outs.append((G, loss, hits))
+    for G, loss, hits in outs[1:]:
+        assert torch.equal(G, outs[0][0]) and torch.equal(loss, outs[0][1])
+        assert torch.equal(hits, outs[0][2])
+
+
 def test_rows_softmax_xent_vs_float64(cuda):
     for M, N in [(1, 1), (9, 3), (1000, 930), (257, 256), (33, 4096), (5, 1025)]:
         L = _rand((M, N), M + N, 3.0)

@@ -30,15 +30,20 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     rows = torch.randint(0, T, (400,), generator=g, device=dev)
     logits64 = P[rows].double() @ W.double() + b.double()
     _, l64, h64, G64 = O.softmax_xent_f64(logits64.cpu().numpy(), y[rows].cpu().numpy(), scale=1.0 / T)
-    err = max(float(np.abs(G[rows].cpu().numpy() - G64).max()) * T,
-              float(np.abs(loss[rows].cpu().numpy() - l64).max()))
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    res = []
-    for _ in range(3):
+    for split in ("0", "4", "8", "16"):
+      os.environ["GCG_GEMM_SPLIT"] = split
+      f()
+      torch.cuda.synchronize()
+      err = max(float(np.abs(G[rows].cpu().numpy() - G64).max()) * T,
+                float(np.abs(loss[rows].cpu().numpy() - l64).max()))
+      res = []
+      for _ in range(3):
         s.record()
         for _ in range(10):
             f()
         e.record()
         torch.cuda.synchronize()
         res.append(round(2.0 * T * K * C / (s.elapsed_time(e) / 10) / 1e9, 1))
-    print(json.dumps({"shape": f"{T}x{K}x{C}", "TFLOPs": res, "max_err": err}), flush=True)
+      print(json.dumps({"shape": f"{T}x{K}x{C}", "split": split, "TFLOPs": res, "max_err": err}),
+            flush=True)
