@@ -728,14 +728,25 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 template <int MG, int NG, int PD>
 __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
     int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
-    int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np) {
+    int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt,
+    int remap) {
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int j = lane & 15, q = lane >> 4;
-  const int m0 = blockIdx.x * (64 * MG);
-  const int n0 = blockIdx.y * (256 * NG) + wave * (64 * NG);
+  // 1-D grid of mt x nt x S tiles, m fastest. remap: XCD-aware bijection (workgroup b runs on
+  // XCD b % 8; each XCD walks one contiguous range of tiles), so the mt x nt tiles of one
+  // split -- which read the same rows of A and B -- share one XCD's L2.
+  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+  int tile = b;
+  if (remap) {
+    const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
+    tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+  }
+  const int bx = tile % mt, by = (tile / mt) % nt, bz = tile / (mt * nt);
+  const int m0 = bx * (64 * MG);
+  const int n0 = by * (256 * NG) + wave * (64 * NG);
   if (n0 >= N) return;  // a wave wholly past N (no LDS, no barriers: safe to leave early)
-  const int t_begin = blockIdx.z * rows_per_split;
+  const int t_begin = bz * rows_per_split;
   const int t_end = min(R, t_begin + rows_per_split);
   const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
   int acol[MG], bcol[NG];
@@ -760,21 +771,26 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
         for (int eb = 0; eb < 4; ++eb) acc[a][b][ea][eb] = f4{0.f, 0.f, 0.f, 0.f};
 
   f4 ra[PD][MG], rb[PD][NG];
+  bool rok[PD];
   auto load = [&](int u, int t0) {
     const int t = t0 + q;
     const bool ok = t < t_end;
-    const int tc = ok ? t : t_begin;  // clamped row, zeroed below
+    const int tc = ok ? t : t_begin;  // clamped row, zeroed at use
     const float* arow = A + static_cast<int64_t>(tc) * lda;
     const float* brow = B + static_cast<int64_t>(tc) * ldb;
+    rok[u] = ok;
 #pragma unroll
-    for (int g = 0; g < MG; ++g) {
-      f4 v = *reinterpret_cast<const f4*>(arow + acol[g]);
-      ra[u][g] = ok ? v : f4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int g = 0; g < MG; ++g) ra[u][g] = *reinterpret_cast<const f4*>(arow + acol[g]);
 #pragma unroll
     for (int g = 0; g < NG; ++g) rb[u][g] = *reinterpret_cast<const f4*>(brow + bcol[g]);
   };
   auto compute = [&](int u) {
+    // Rows past the split are zeroed here, at use, not at load: a select right after the load
+    // makes hipcc wait for it there, draining the PD-deep ring every step (round 2: ISA showed
+    // vmcnt(0)/(1) before every step's MFMAs).
+    f4 av[MG];
+#pragma unroll
+    for (int a = 0; a < MG; ++a) av[a] = rok[u] ? ra[u][a] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < MG; ++a)
 #pragma unroll
@@ -783,20 +799,28 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
         for (int ea = 0; ea < 4; ++ea)
 #pragma unroll
           for (int eb = 0; eb < 4; ++eb)
-            acc[a][b][ea][eb] = mfma4(ra[u][a][ea], rb[u][b][eb], acc[a][b][ea][eb]);
+            acc[a][b][ea][eb] = mfma4(av[a][ea], rb[u][b][eb], acc[a][b][ea][eb]);
   };
   // steps of 4 rows; the ring is refilled PD steps ahead (loads past t_end are zeroed)
 #pragma unroll
-  for (int u = 0; u < PD; ++u) load(u, t_begin + 4 * u);
+  for (int u = 0; u < PD; ++u) {
+    load(u, t_begin + 4 * u);
+    __builtin_amdgcn_sched_barrier(0);  // issue order = ring order (counted waits below)
+  }
+  // The scheduling barriers pin each refill behind its step's MFMAs: without them the machine
+  // scheduler sinks every load next to its use (to cut register pressure) and the ring is gone
+  // -- one exposed load latency per step (round 2, ISA: vmcnt(0) before each step's MFMAs).
   for (int t0 = t_begin; t0 < t_end; t0 += 4 * PD) {
 #pragma unroll
     for (int u = 0; u < PD; ++u) {
       compute(u);
+      __builtin_amdgcn_sched_barrier(0);
       load(u, t0 + 4 * (u + PD));
+      __builtin_amdgcn_sched_barrier(0);
     }
   }
   // partial tile: lane holds C[m0 + 64a + 16q + 4r + ea][n0 + 64b + 4j + eb] in acc[a][b][ea][eb][r]
-  float* dst = part + static_cast<int64_t>(blockIdx.z) * Mp * Np;
+  float* dst = part + static_cast<int64_t>(bz) * Mp * Np;
 #pragma unroll
   for (int a = 0; a < MG; ++a)
 #pragma unroll
@@ -1246,17 +1270,20 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
                 need);
   if (!aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace not 16-B aligned", fn);
   float* part = static_cast<float*>(workspace);
-  const dim3 grid(p.mt, p.nt, p.S);
+  const int64_t n_tiles = int64_t{p.mt} * p.nt * p.S;
+  if (n_tiles > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "%s: too many tiles", fn);
+  const dim3 grid(static_cast<unsigned>(n_tiles));
+  const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
+  const int remap = rmv ? std::atoi(rmv) : 1;
 #define GCG_TN_CASE(MG_, NG_, PD_)                                                           \
   if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_) {                                           \
     hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_>), grid, dim3(256), 0, s, int(R),\
-                       int(M), int(N), A, lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np);  \
+                       int(M), int(N), A, lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np,   \
+                       p.mt, p.nt, remap);                                                   \
   } else
   GCG_TN_CASE(1, 2, 4)
   GCG_TN_CASE(1, 2, 8)
   GCG_TN_CASE(1, 1, 8)
-  GCG_TN_CASE(1, 2, 12)
-  GCG_TN_CASE(1, 2, 16)
   GCG_TN_CASE(1, 1, 16)
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
 #undef GCG_TN_CASE

@@ -50,7 +50,7 @@ def main():
     ap.add_argument("--classes", type=int, default=930)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--tiles", default="rt2,rt4,8w,occ2", help="wide-tile variants to compare")
-    ap.add_argument("--tn", default="1:2:8,1:2:12,1:2:16,1:1:16", help="TN tile variants")
+    ap.add_argument("--tn", default="1:2:8,1:2:4,1:1:8,1:1:16", help="TN tile variants")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     T, N, K, C = args.rows, args.nodes, args.hidden, args.classes
