@@ -1,14 +1,11 @@
 #!/bin/bash
 # Train-step evidence (BASELINE config 3 and the Twitter-World step): bench_train.py JSON lines
-# plus rocprofv3 kernel-trace stats of the same command, both layer-2 orders; and the fused
-# output-layer tile experiment.
+# plus rocprofv3 kernel-trace stats of the same command, both layer-2 orders.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 out=gpurun_out/train_prof
 mkdir -p $out
-timeout -k 10 200 python -u tools/exp_fused_rt.py > $out/fused_rt.log 2>&1 || { tail -5 $out/fused_rt.log; exit 1; }
-grep '^{' $out/fused_rt.log
 for cfg in twitter-us twitter-world; do for order in reference propagate_first; do
 tag=${cfg}_${order}
 timeout -k 10 300 python -u tools/bench_train.py --config $cfg --order $order > $out/$tag.json.log 2>&1 || { tail -20 $out/$tag.json.log; exit 1; }
