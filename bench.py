@@ -35,6 +35,7 @@ from graphconvgeo_amd.synth import CONFIGS, SEED, synthetic_graph  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md:296, "~6.3 TB/s achievable"
+MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (v_mfma_f32_16x16x4_f32) at 2.4 GHz
 
 
 def spmm_bytes(n_rows: int, nnz: int, K: int) -> int:
@@ -206,6 +207,45 @@ def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev) -> dict:
     return rec
 
 
+def dense_kernels_bench(reps: int, dev) -> dict:
+    """The output layer's MFMA kernels (T.dot(h, W2) + b2, softmax-CE and their gradients,
+    mlpconv.py:88-95) at Twitter-World's shapes -- 840k target rows x K=300 x C=930 -- each
+    timed alone with HIP events (mean of `reps` launches after one warm-up), TFLOP/s against
+    the dense f32 MFMA peak. Random data; parity is in tests/test_dense_gpu.py."""
+    import math
+
+    from graphconvgeo_amd import dense
+    T, K, C = 840_000, 300, 930
+    g = torch.Generator(device=dev).manual_seed(SEED + 21)
+    P = gs.empty_dense(T, K, dev).copy_(torch.randn((T, K), generator=g, device=dev) * 0.1)
+    W = (torch.rand((K, C), generator=g, device=dev) * 2 - 1) * math.sqrt(6.0 / (K + C))
+    b = torch.randn(C, generator=g, device=dev) * 0.01
+    y = torch.randint(0, C, (T,), generator=g, device=dev, dtype=torch.int32)
+    W_kc = dense._WeightCache().get(W, False)  # [K][round4(C)]: fused layer / dgrad operand
+    W_ck = dense._WeightCache().get(W, True)   # [C][round4(K)]: NT forward operand
+    G = gs.empty_dense(T, C, dev)
+    dP = gs.empty_dense(T, K, dev)
+    loss = torch.empty(T, device=dev)
+    hits = torch.empty(T, device=dev)
+    kernels = {
+        "gemm_nt: P.W2 + b2 (mlpconv.py:88)": lambda: dense.gemm_nt(P, W_ck, bias=b, out=G),
+        "gemm_nt: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP),
+        "gemm_tn: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G),
+        "fused: P.W2 + b2 -> softmax-CE, hits, dlogits (mlpconv.py:88-95)":
+            lambda: dense._fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits),
+    }
+    flops = 2.0 * T * K * C
+    out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS}
+    for name, fn in kernels.items():
+        fn()
+        ms = time_events(fn, reps, dev)
+        tf = flops / (ms * 1e-3) / 1e12
+        out[name] = {"ms": round(ms, 3), "TFLOPs": round(tf, 1),
+                     "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 3)}
+    del P, G, dP, W_kc, W_ck
+    return out
+
+
 def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -> dict:
     """BASELINE config 3: one MLPCONV epoch (mlpconv.py:293-295 -> f_train: 2-layer GCN
     forward + backward + Lasagne Adam, tensormain.py:232-237) at Twitter-US scale on one GPU,
@@ -308,6 +348,8 @@ def main():
                     help="N = 1: skip the uniform-degree second run")
     ap.add_argument("--no-train-step", dest="train_step", action="store_false",
                     help="N = 1: skip the config-3 (Twitter-US) training-step measurement")
+    ap.add_argument("--no-dense", dest="dense", action="store_false",
+                    help="N = 1: skip timing the output layer's MFMA kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--chunks", type=int, default=2,
                     help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
@@ -509,6 +551,8 @@ def main():
         del Z, Y
         rec["variants"] = {"uniform": spmm_variant(cfg, "uniform", K, args.mode,
                                                    max(args.steps, 5), dev)}
+    if world == 1 and not args.partitioned and args.dense:
+        rec["dense_kernels"] = dense_kernels_bench(max(args.steps // 2, 5), dev)
     if world == 1 and not args.partitioned and args.train_step:
         # BASELINE config 3: Twitter-US 2-layer fwd+bwd step (both layer-2 orders)
         rec["train_step"] = train_step_bench(max(args.steps // 2, 5), max(args.warmup, 2), dev)
