@@ -246,6 +246,23 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     return out
 
 
+def spmm_wide_variant(A, N: int, nnz: int, K: int, mode: str, reps: int, dev) -> dict:
+    """the same World SpMM at the wider hidden size K = 1500
+    (tensormain.py:398), on the headline graph already resident in HBM."""
+    g = torch.Generator(device=dev).manual_seed(SEED + 13)
+    Z = torch.randn((N, K), generator=g, device=dev)
+    Y = gs.empty_dense(N, K, dev)
+    gs.spmm(A, Z, out=Y, mode=mode)
+    k_ms = time_events(lambda: gs.spmm(A, Z, out=Y, mode=mode), reps, dev)
+    B = spmm_bytes(N, nnz, K)
+    gbs = B / (k_ms * 1e-3) / 1e9
+    del Z, Y
+    return {"graph": "powerlaw (the headline graph)", "K": K, "mode": mode,
+            "kernel_ms": round(k_ms, 3), "value": round(gbs, 1), "unit": "GB/s",
+            "edges_per_s": round(nnz / (k_ms * 1e-3), 1), "frac": round(gbs / HBM_PEAK_GBS, 4),
+            "algorithmic_bytes_per_launch": B}
+
+
 def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -> dict:
     """BASELINE config 3: one MLPCONV epoch (mlpconv.py:293-295 -> f_train: 2-layer GCN
     forward + backward + Lasagne Adam, tensormain.py:232-237) at Twitter-US scale on one GPU,
@@ -551,6 +568,9 @@ def main():
         del Z, Y
         rec["variants"] = {"uniform": spmm_variant(cfg, "uniform", K, args.mode,
                                                    max(args.steps, 5), dev)}
+        if args.graph == "powerlaw" and K != 1500:
+            rec["variants"]["k1500"] = spmm_wide_variant(A, N, nnz, 1500, eff,
+                                                         max(args.steps // 4, 3), dev)
     if world == 1 and not args.partitioned and args.dense:
         rec["dense_kernels"] = dense_kernels_bench(max(args.steps // 2, 5), dev)
     if world == 1 and not args.partitioned and args.train_step:

@@ -41,7 +41,7 @@ def test_bench_single_gpu_line(cuda):
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
     rf = rec["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["frac_vs_achievable"] > 0
-    assert rec["variants"]["uniform"]["kernel_ms"] > 0
+    assert rec["variants"]["uniform"]["kernel_ms"] > 0 and rec["variants"]["k1500"]["kernel_ms"] > 0
     dk = {k: v for k, v in rec["dense_kernels"].items() if isinstance(v, dict)}
     assert len(dk) == 4 and all(v["TFLOPs"] > 0 and v["frac"] < 1 for v in dk.values())
 
