@@ -488,6 +488,8 @@ def main():
                         compulsory_bytes(part.n_local, part.nnz_local, K, part.operand_rows()))}
         if traffic_src:
             roofline["traffic_source"] = traffic_src
+        if 4 * K * N <= 256 * 2**20:  # the dense operand fits the Infinity Cache
+            roofline["note"] = "cache-resident, not roofline-bound (Z fits the 256 MB Infinity Cache)"
         if kbytes != B:
             roofline["scope"] = f"rank {rank} local SpMM ({part.n_local} rows, {part.nnz_local} nnz)"
 
