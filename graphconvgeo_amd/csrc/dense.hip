@@ -115,7 +115,11 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   // (a branchy load makes it drain every load in flight). A 16-B load at a clamped column
   // stays inside the 16-B aligned block of a valid element, hence inside the allocation.
   const int kmax4 = (K - 1) & ~3;  // last 4-aligned column start with a valid element
+  // The out-of-range elements are zeroed when the registers are written to LDS (store_a), not
+  // right after the load: a select on the loaded value makes hipcc wait for the load there,
+  // at the top of the chunk, instead of at the chunk's end.
   f4 areg[A4];
+  int avalid[A4];  // valid elements of areg[i]: 0..4 (0 for a row past M)
   auto load_a = [&](int kc0) {
 #pragma unroll
     for (int i = 0; i < A4; ++i) {
@@ -124,13 +128,8 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
       const int64_t gr = row0 + r;
       const int64_t rr = gr < M ? gr : M - 1;
       const int kk = k < kmax4 ? k : kmax4;
-      f4 v = *reinterpret_cast<const f4*>(A + rr * lda + kk);
-      const bool rowok = gr < M;
-      v.x = (rowok && k < K) ? v.x : 0.f;
-      v.y = (rowok && k + 1 < K) ? v.y : 0.f;
-      v.z = (rowok && k + 2 < K) ? v.z : 0.f;
-      v.w = (rowok && k + 3 < K) ? v.w : 0.f;
-      areg[i] = v;
+      areg[i] = *reinterpret_cast<const f4*>(A + rr * lda + kk);
+      avalid[i] = gr < M ? min(max(K - k, 0), 4) : 0;
     }
   };
   auto store_a = [&](int buf) {
@@ -138,7 +137,12 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
     for (int i = 0; i < A4; ++i) {
       const int idx = tid + NT * i;
       const int r = idx / (KC / 4), k4 = (idx % (KC / 4)) * 4;
-      *reinterpret_cast<f4*>(&As[buf][r][k4]) = areg[i];
+      f4 v = areg[i];
+      v.x = avalid[i] > 0 ? v.x : 0.f;
+      v.y = avalid[i] > 1 ? v.y : 0.f;
+      v.z = avalid[i] > 2 ? v.z : 0.f;
+      v.w = avalid[i] > 3 ? v.w : 0.f;
+      *reinterpret_cast<f4*>(&As[buf][r][k4]) = v;
     }
   };
   // Workgroup barrier for the LDS hand-off only: waits for this wave's LDS traffic, not for
@@ -210,8 +214,10 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
     // per CU). Every accumulator still sees e = 0..3 in order: bitwise equal to PF = 0.
     constexpr int NP = PF, NU = 4 * G;
     static_assert(NU % NP == 0, "parts split the fragments evenly");
-    // (Pinning the issue order with sched barriers, as gemm_tn_partial_kernel does, measured
-    // 93.0-95.0 vs 96.2 TFLOP/s here: not used.)
+    // (hipcc still drains most of the ring at the loop header -- vmcnt(2) before the first
+    // part's MFMAs -- when it merges the preheader's and the back-edge's outstanding loads;
+    // pinning the issue order with scheduling barriers, as gemm_tn_partial_kernel does, did
+    // not change that here and measured 93.0-95.0 vs 96.2 TFLOP/s in the loop body.)
 #pragma unroll
     for (int p = 0; p < NP; ++p) load_b(b0, 0, p * NU / NP, (p + 1) * NU / NP);
     for (int c = 0; c < n_chunks; ++c) {
@@ -219,12 +225,16 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
       const int k0 = c * KC;
       load_a(k0 + KC);  // past K: clamped and zeroed, never used
 #pragma unroll
-      for (int st = 0; st < 2; ++st)  // k0 + 16 >= K: A is zero there
+      for (int st = 0; st < 2; ++st) {
+        // the second 16-deep step of the last chunk lies wholly past K (A is zero there):
+        // skip its MFMAs and the refills, which would only fetch rows past K
+        if (st == 1 && k0 + 16 >= K) break;
 #pragma unroll
         for (int p = 0; p < NP; ++p) {
           compute(b0, buf, st, p * NU / NP, (p + 1) * NU / NP);
           load_b(b0, k0 + 16 * (st + 1), p * NU / NP, (p + 1) * NU / NP);
         }
+      }
       store_a(buf ^ 1);
       lds_barrier();
     }
