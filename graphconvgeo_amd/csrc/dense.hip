@@ -201,6 +201,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   // ahead), A chunk c+1 is loaded to registers during chunk c and written to the other LDS
   // buffer after it.
   static_assert(KC == 32, "two 16-deep steps per chunk");
+  __builtin_assume(K > 0);  // checked on the host: the main loop runs at least once
   const int n_chunks = (K + KC - 1) / KC;
   load_a(0);
   store_a(0);
@@ -214,12 +215,17 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
     // per CU). Every accumulator still sees e = 0..3 in order: bitwise equal to PF = 0.
     constexpr int NP = PF, NU = 4 * G;
     static_assert(NU % NP == 0, "parts split the fragments evenly");
-    // (hipcc still drains most of the ring at the loop header -- vmcnt(2) before the first
-    // part's MFMAs -- when it merges the preheader's and the back-edge's outstanding loads;
-    // pinning the issue order with scheduling barriers, as gemm_tn_partial_kernel does, did
-    // not change that here and measured 93.0-95.0 vs 96.2 TFLOP/s in the loop body.)
+    // The prologue issues the parts in ring order (scheduling barriers; K > 0 is assumed so
+    // the loads are not sunk past a zero-trip branch): hipcc merges the preheader's and the
+    // back-edge's outstanding loads at the loop header and otherwise drains the ring there
+    // (vmcnt(2)); now every wait is counted (vmcnt(15..16)). Measured neutral (the kernel runs
+    // at a power-limited clock), kept for the cleaner schedule. Pinning the loop body as well
+    // measured slower: 93.0-95.0 vs 96.2 TFLOP/s.
 #pragma unroll
-    for (int p = 0; p < NP; ++p) load_b(b0, 0, p * NU / NP, (p + 1) * NU / NP);
+    for (int p = 0; p < NP; ++p) {
+      load_b(b0, 0, p * NU / NP, (p + 1) * NU / NP);
+      __builtin_amdgcn_sched_barrier(0);
+    }
     for (int c = 0; c < n_chunks; ++c) {
       const int buf = c & 1;
       const int k0 = c * KC;
