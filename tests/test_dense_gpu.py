@@ -88,7 +88,8 @@ def test_gemm_rejects_bad_operands(cuda):
 
 
 @pytest.mark.parametrize("M,K,N", [(1, 4, 2), (37, 16, 129), (300, 300, 256), (513, 300, 930),
-                                   (64, 65, 1024), (20, 3, 61), (40, 50, 300), (33, 70, 700)])
+                                   (64, 65, 1024), (20, 3, 61), (40, 50, 300), (33, 70, 700),
+                                   (20, 16, 700), (9, 4, 520)])
 def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
     P, W, b = _rand((M, K), 11, 0.3), _rand((K, N), 12, 0.3), _rand((N,), 13)
     y = np.random.default_rng(14).integers(0, N, M).astype(np.int32)
