@@ -211,7 +211,8 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     """The output layer's MFMA kernels (T.dot(h, W2) + b2, softmax-CE and their gradients,
     mlpconv.py:88-95) at Twitter-World's shapes -- 840k target rows x K=300 x C=930 -- each
     timed alone with HIP events (mean of `reps` launches after one warm-up), TFLOP/s against
-    the dense f32 MFMA peak. Random data; parity is in tests/test_dense_gpu.py."""
+    the dense f32 MFMA peak (steady state: 5 untimed launches first). Random data; parity is
+    in tests/test_dense_gpu.py."""
     import math
 
     from graphconvgeo_amd import dense
@@ -237,7 +238,8 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     flops = 2.0 * T * K * C
     out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS}
     for name, fn in kernels.items():
-        fn()
+        for _ in range(5):  # the first launches after a switch run while the clock ramps
+            fn()
         ms = time_events(fn, reps, dev)
         tf = flops / (ms * 1e-3) / 1e12
         out[name] = {"ms": round(ms, 3), "TFLOPs": round(tf, 1),

@@ -579,6 +579,23 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
 
+  // bias of this lane's output columns, loaded now so its latency hides behind the K loop
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bv[g] = f4{0.f, 0.f, 0.f, 0.f};
+    const int c = colw + 64 * g + 4 * j;
+    if (bias != nullptr) {
+      if (c + 3 < N) {
+        bv[g] = f4{bias[c], bias[c + 1], bias[c + 2], bias[c + 3]};
+      } else {
+        if (c < N) bv[g].x = bias[c];
+        if (c + 1 < N) bv[g].y = bias[c + 1];
+        if (c + 2 < N) bv[g].z = bias[c + 2];
+      }
+    }
+  }
+
   const int n_chunks = (K + KC - 1) / KC;
   const int arow0 = wr * 16 * RT + j;       // A image row of tile 0 (lane j)
   const int brow0 = BM + wc * G * 64 + j;   // B image row of group 0, tile e = 0 (lane j)
@@ -655,7 +672,9 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       }
     }
   }
+#define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
+#undef GCG_EPI_BV_READY
 }
 
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
