@@ -345,9 +345,7 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
 
 
 def resolve_mode(A, mode: str) -> str:
-    if mode != "auto":
-        return mode
-    return "ordered" if A.max_row_nnz() * gs.AUTO_SPLIT_RATIO <= max(A.nnz, 1) else "fast"
+    return mode if mode != "auto" else gs.resolve_auto(A)
 
 
 def main():

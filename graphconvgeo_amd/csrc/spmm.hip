@@ -342,6 +342,11 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
     if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
     if (inflight != 64 && a.task_nnz >= 256) return launch_rows_f<4, 2, 192>(a, n_panels, stream);
+    // plan-less, one row per wave, on a large graph (sparse.resolve_auto picks it for graphs
+    // without hub rows): U = 16, 3 waves/SIMD -- Twitter-World uniform 9.35-9.36 vs 9.41-9.44 ms
+    // at U = 8 (two boxes)
+    if (inflight != 64 && a.tasks == nullptr && a.n_tasks >= 65536)
+      return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
   }
   launch_rows_f<VEC, NCH, 64>(a, n_panels, stream);
 }

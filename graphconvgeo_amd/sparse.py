@@ -31,6 +31,23 @@ MODES = ("auto", "fast", "ordered", "rowwise")
 # whole launch (then rows are split, 'fast'): longest-first scheduling hides a row of up
 # to ~nnz/2048 nonzeros behind the bulk (Twitter-World: 12,189 of 41.4M, measured equal).
 AUTO_SPLIT_RATIO = 2048
+# ... and the plan-less 'rowwise' form (also bitwise) when no row is a hub: longest row at most
+# AUTO_ROWWISE_SKEW x the mean, on a graph large enough to fill the chip with one wave per row.
+# Measured on the Twitter-World uniform-degree graph (max 2.2x the mean), K = 300: 9.43 vs
+# 9.63 ms for the 512-nnz task plan; on the power-law graph rowwise is 18 % slower (hub rows).
+AUTO_ROWWISE_SKEW = 4
+AUTO_ROWWISE_MIN_ROWS = 65536
+
+
+def resolve_auto(A) -> str:
+    """The mode 'auto' runs on A: 'fast', 'rowwise' or 'ordered' (see above)."""
+    longest, nnz = A.max_row_nnz(), max(A.nnz, 1)
+    if longest * AUTO_SPLIT_RATIO > nnz:
+        return "fast"
+    if A.n_rows >= AUTO_ROWWISE_MIN_ROWS and longest * A.n_rows <= AUTO_ROWWISE_SKEW * nnz:
+        return "rowwise"
+    return "ordered"
+
 # DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
 # the dense MFMA GEMM -- break-even is ~1.5-2 % (a gathered nonzero ~190 ps, a dense element
 # ~3-9 ps at Twitter-World, tools/exp_xtg_head.py / exp_tn_shapes.py); at most HYBRID_MAX_COLS
@@ -379,7 +396,8 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
          gate: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Y = act(A . Z + bias)[rows] on the GPU (S.dot of mlpconv.py:71,73,90 + epilogue).
 
-    mode  'auto'    : 'ordered' unless the longest row could outlast the launch, then 'fast'
+    mode  'auto'    : 'ordered' unless the longest row could outlast the launch, then 'fast';
+                      'rowwise' on large graphs without hub rows (resolve_auto)
           'fast'    : planned; rows longer than task_nnz split across waves (|err| <= 1e-5)
           'ordered' : planned, rows never split -> bitwise scipy float32
           'rowwise' : plan-less, one wave per output row -> bitwise scipy float32
@@ -445,7 +463,7 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
     stream = _stream_handle(A.device)
     actc = ACTS[act]
     if mode == "auto":
-        mode = "ordered" if A.max_row_nnz() * AUTO_SPLIT_RATIO <= max(A.nnz, 1) else "fast"
+        mode = resolve_auto(A)
     with torch.cuda.device(A.device):
         if mode == "rowwise":
             call("gcg_spmm_csr_f32_gate", A.n_rows, A.n_cols, A.nnz, _ptr(A.indptr),
