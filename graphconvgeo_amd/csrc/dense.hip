@@ -83,6 +83,10 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   static_assert(A4 >= 1 && BM * KC / 4 % NT == 0, "A chunk must split evenly");
   __shared__ float As[2][BM][KP];
   __shared__ float red[3][WC][BM];
+  // EPI = 1: the bias of the workgroup's columns and the labels of its rows, staged in LDS
+  // at the start so the epilogue reads them from LDS instead of waiting on global loads
+  __shared__ float sbias[EPI == 1 ? BN : 1];
+  __shared__ int slab[EPI == 1 ? BM : 1];
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -204,6 +208,20 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   __builtin_assume(K > 0);  // checked on the host: the main loop runs at least once
   const int n_chunks = (K + KC - 1) / KC;
   load_a(0);
+  if constexpr (EPI == 1) {
+    for (int c = tid; c < BN; c += NT) {
+      const int gc = blockIdx.y * BN + c;
+      sbias[c] = (bias != nullptr && gc < N) ? bias[gc] : 0.f;
+    }
+    for (int r = tid; r < BM; r += NT) {
+      const int64_t row = row0 + r;
+      int y = (labels != nullptr && row < M) ? labels[row] : -1;
+      // -1: no label; a label outside [0, N) becomes -2: NaN loss, no hit, no onehot
+      if (labels != nullptr && (y < 0 || y >= N)) y = -2;
+      slab[r] = y;
+    }
+    // (issued beside the first A chunk's loads; visible after the barrier below)
+  }
   store_a(0);
   lds_barrier();
   f4 b0[G][4];
@@ -276,7 +294,27 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
     }
   }
 
+#define GCG_EPI_BV_READY
+#define GCG_EPI_LABELS_LDS
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    if constexpr (EPI == 1) {
+      bv[g] = *reinterpret_cast<const f4*>(&sbias[wc * G * 64 + 64 * g + 4 * j]);
+    } else {
+      bv[g] = f4{0.f, 0.f, 0.f, 0.f};
+      const int c = colw + 64 * g + 4 * j;
+      if (bias != nullptr) {
+        if (c < N) bv[g].x = bias[c];
+        if (c + 1 < N) bv[g].y = bias[c + 1];
+        if (c + 2 < N) bv[g].z = bias[c + 2];
+        if (c + 3 < N) bv[g].w = bias[c + 3];
+      }
+    }
+  }
 #include "gemm_epilogue.inc"
+#undef GCG_EPI_BV_READY
+#undef GCG_EPI_LABELS_LDS
 }
 
 // ---------------------------------------------------------------------------------------
