@@ -82,7 +82,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   constexpr int A4 = BM * KC / 4 / NT;     // A dwordx4 per thread per chunk
   static_assert(A4 >= 1 && BM * KC / 4 % NT == 0, "A chunk must split evenly");
   __shared__ float As[2][BM][KP];
-  __shared__ float red[3][WC][BM];
+  __shared__ float red[4][WC][BM];  // epilogue row reductions: sum, label logit, argmax, max
   // EPI = 1: the bias of the workgroup's columns and the labels of its rows, staged in LDS
   // at the start so the epilogue reads them from LDS instead of waiting on global loads
   __shared__ float sbias[EPI == 1 ? BN : 1];
@@ -348,10 +348,10 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
   static_assert(BN % 16 == 0, "conflict-free B fragment reads");
   // NB = 2 LDS buffers (one barrier per chunk) for the 8-wave tiles, which hold a CU alone
   // anyway; the 4-wave tiles keep one buffer (two barriers) so 2-3 workgroups share a CU
-  constexpr int NB = (WC >= 2 && (2 * (BM * KP + KC * BN) + 3 * WC * BM) * 4 <= 160 * 1024) ? 2 : 1;
+  constexpr int NB = (WC >= 2 && (2 * (BM * KP + KC * BN) + 4 * WC * BM) * 4 <= 160 * 1024) ? 2 : 1;
   __shared__ float As[NB][BM][KP];
   __shared__ float Bs[NB][KC][BN];
-  __shared__ float red[3][WC][BM];
+  __shared__ float red[4][WC][BM];  // epilogue row reductions: sum, label logit, argmax, max
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
