@@ -51,6 +51,9 @@ SIGNATURES = {
                                      _i64, _pi64, _pi64]),
     "gcg_adam_step_f32": (C.c_int, [_i64, _p, _p, _p, _p, _p, C.c_float, C.c_float, C.c_float,
                                     _p]),
+    "gcg_l1l2_penalty_f32": (C.c_int, [_i64, _p, C.c_float, C.c_float, _p, _p, _p, C.c_size_t,
+                                       _p]),
+    "gcg_l1l2_grad_f32": (C.c_int, [_i64, _p, C.c_float, C.c_float, _p, _p, _p]),
     "gcg_csr_validate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p]),
     "gcg_index_csr": (C.c_int, [_i64, _p, _i64, _p, _p, _p, C.c_size_t, _psz, _p]),
     "gcg_scatter_add_rows_f32": (C.c_int, [_i64, _p, _p, _p, _i64, _i64, _p, _i64, _p]),

@@ -237,6 +237,67 @@ __global__ __launch_bounds__(256) void adam_kernel(int64_t n, float* __restrict_
   }
 }
 
+// lasagne.regularization l1 / l2 of one weight (mlpconv.py:235-243): partial sums of |w| and
+// w*w over a fixed grid (kPenBlocks blocks, grid-stride order fixed by the grid), one pair per
+// block; then ONE thread adds the pairs in block order -- deterministic, graph-capturable.
+constexpr int kPenBlocks = 256;
+
+__global__ __launch_bounds__(256) void l1l2_partial_kernel(int64_t n, const float* __restrict__ w,
+                                                           float* __restrict__ part) {
+  __shared__ float s1[256], s2[256];
+  float a = 0.f, q = 0.f;
+  const int64_t stride = static_cast<int64_t>(kPenBlocks) * 256;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x; i < n; i += stride) {
+    const float x = w[i];
+    a += fabsf(x);
+    q += x * x;
+  }
+  s1[threadIdx.x] = a;
+  s2[threadIdx.x] = q;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if (static_cast<int>(threadIdx.x) < h) {
+      s1[threadIdx.x] += s1[threadIdx.x + h];
+      s2[threadIdx.x] += s2[threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = s1[0];
+    part[2 * blockIdx.x + 1] = s2[0];
+  }
+}
+
+// out = ((acc_in ? *acc_in : 0) + l1 * sum|w|) + l2 * sum w^2 (acc_in may alias out).
+__global__ __launch_bounds__(64) void l1l2_finish_kernel(const float* __restrict__ part, float l1,
+                                                         float l2, const float* acc_in,
+                                                         float* out) {
+  if (threadIdx.x != 0) return;
+  float a = 0.f, q = 0.f;
+  for (int b = 0; b < kPenBlocks; ++b) {
+    a += part[2 * b];
+    q += part[2 * b + 1];
+  }
+  const float base = acc_in != nullptr ? *acc_in : 0.f;
+  out[0] = (base + a * l1) + q * l2;
+}
+
+// d/dw of l1 * sum|w| + l2 * sum w^2, times the upstream gradient: s * (l1 sgn(w) + 2 l2 w)
+// (Theano's grad of abs is sgn, 0 at 0).
+__global__ __launch_bounds__(256) void l1l2_grad_kernel(int64_t n, const float* __restrict__ w,
+                                                        float l1, float l2,
+                                                        const float* __restrict__ scale_dev,
+                                                        float* __restrict__ dw) {
+  const float s = scale_dev != nullptr ? *scale_dev : 1.0f;
+  const float c1 = s * l1, c2 = s * (2.0f * l2);
+  const int64_t stride = static_cast<int64_t>(gridDim.x) * blockDim.x;
+  for (int64_t i = static_cast<int64_t>(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += stride) {
+    const float x = w[i];
+    const float sg = x > 0.f ? 1.f : (x < 0.f ? -1.f : 0.f);
+    dw[i] = c1 * sg + c2 * x;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -250,6 +311,33 @@ gcg_status gcg_adam_step_f32(int64_t n, float* p, const float* g, float* m, floa
   if (n == 0) return GCG_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(grid_for(n)), dim3(256), 0, static_cast<hipStream_t>(stream),
                      n, p, g, m, v, step_dev, beta1, beta2, eps);
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+gcg_status gcg_l1l2_penalty_f32(int64_t n, const float* W, float l1, float l2,
+                                const float* acc_in, float* out, void* workspace,
+                                size_t workspace_bytes, gcg_stream_t stream) {
+  if (n < 0 || (n > 0 && W == nullptr) || out == nullptr || workspace == nullptr)
+    return fail(GCG_ERR_INVALID_ARG, "gcg_l1l2_penalty_f32: bad arguments");
+  if (workspace_bytes < GCG_L1L2_WORKSPACE_BYTES || !aligned(workspace, 4))
+    return fail(GCG_ERR_INVALID_ARG, "gcg_l1l2_penalty_f32: workspace needs %d aligned bytes",
+                GCG_L1L2_WORKSPACE_BYTES);
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  float* part = static_cast<float*>(workspace);
+  hipLaunchKernelGGL(l1l2_partial_kernel, dim3(kPenBlocks), dim3(256), 0, st, n, W, part);
+  hipLaunchKernelGGL(l1l2_finish_kernel, dim3(1), dim3(64), 0, st, part, l1, l2, acc_in, out);
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+gcg_status gcg_l1l2_grad_f32(int64_t n, const float* W, float l1, float l2,
+                             const float* scale_dev, float* dW, gcg_stream_t stream) {
+  if (n < 0 || (n > 0 && (W == nullptr || dW == nullptr)))
+    return fail(GCG_ERR_INVALID_ARG, "gcg_l1l2_grad_f32: bad arguments");
+  if (n == 0) return GCG_OK;
+  hipLaunchKernelGGL(l1l2_grad_kernel, dim3(grid_for(n)), dim3(256), 0,
+                     static_cast<hipStream_t>(stream), n, W, l1, l2, scale_dev, dW);
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }

@@ -236,6 +236,20 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     return;
   }
 
+  // The bias depends on the column only: loaded once per wave, before the row loop. (Loaded
+  // after each row's gathers it was a dependent global load per row: +8 % on Twitter-US
+  // H.Z1 + b1, +5 % at World.)
+  Vec<VEC> bv[NCH];
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    if (bias != nullptr) {
+      bv[k] = load_vec<VEC>(bias + gcol[k]);
+    } else {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) bv[k].x[q] = 0.0f;
+    }
+  }
+
   for (int p = t.x; p < t.y; ++p) {
     const int r = out_rows ? uniform(out_rows[p]) : p;
     const int s = uniform(indptr[r]);
@@ -250,9 +264,8 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     for (int k = 0; k < NCH; ++k) {
       if (!on[k]) continue;
       if (bias != nullptr) {
-        const Vec<VEC> b = load_vec<VEC>(bias + col[k]);
 #pragma unroll
-        for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + b.x[q];
+        for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + bv[k].x[q];
       }
       if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], acc[k]);
 #pragma unroll

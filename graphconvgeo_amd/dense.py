@@ -487,6 +487,57 @@ def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int
     return _SoftmaxXent.apply(logits, labels, denom)
 
 
+L1L2_WORKSPACE_BYTES = 2048  # GCG_L1L2_WORKSPACE_BYTES
+
+
+class _L1L2Penalty(torch.autograd.Function):
+    """sum_i l1_i * sum|W_i| + l2_i * sum W_i^2, added up in the order of the weights: two
+    launches per weight forward (gcg_l1l2_penalty_f32), one per weight backward
+    (gcg_l1l2_grad_f32, the upstream gradient read on the device), instead of ~20 elementwise
+    and reduction torch kernels for the penalty and its gradient per training step."""
+
+    @staticmethod
+    def forward(ctx, coefs, *weights):
+        dev = weights[0].device
+        out = torch.empty((), dtype=torch.float32, device=dev)
+        ws = torch.empty(L1L2_WORKSPACE_BYTES // 4, dtype=torch.float32, device=dev)
+        acc = None
+        with torch.cuda.device(dev):
+            for W, (l1, l2) in zip(weights, coefs):
+                call("gcg_l1l2_penalty_f32", W.numel(), _ptr(W), float(l1), float(l2), _ptr(acc),
+                     _ptr(out), _ptr(ws), L1L2_WORKSPACE_BYTES, _stream_handle(dev))
+                acc = out
+        ctx.coefs = coefs
+        ctx.save_for_backward(*weights)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.reshape(1).to(torch.float32).contiguous()
+        grads = []
+        for i, (W, (l1, l2)) in enumerate(zip(ctx.saved_tensors, ctx.coefs)):
+            if not ctx.needs_input_grad[1 + i]:
+                grads.append(None)
+                continue
+            dW = torch.empty_like(W)
+            with torch.cuda.device(W.device):
+                call("gcg_l1l2_grad_f32", W.numel(), _ptr(W), float(l1), float(l2), _ptr(g),
+                     _ptr(dW), _stream_handle(W.device))
+            grads.append(dW)
+        return (None, *grads)
+
+
+def l1l2_penalty(weights, coefs) -> torch.Tensor:
+    """The MLPCONV weight penalty (mlpconv.py:235-243): sum over the weights, in the given
+    order, of l1 * sum|W| + l2 * sum W^2 (l1 = regul_coef * l1_share, l2 = regul_coef *
+    (1 - l1_share)), differentiable in every weight; deterministic. Device scalar."""
+    for W in weights:
+        _require_cuda(W, "W")
+        if W.dtype != torch.float32 or not W.is_contiguous():
+            raise TypeError("l1l2_penalty needs contiguous float32 weights")
+    return _L1L2Penalty.apply(tuple((float(a), float(b)) for a, b in coefs), *weights)
+
+
 def softmax(logits: torch.Tensor) -> torch.Tensor:
     """Row softmax (predict_proba) through the row kernel."""
     _require_cuda(logits, "logits")

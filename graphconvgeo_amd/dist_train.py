@@ -185,9 +185,8 @@ class RowPartitionedGCN:
             loss, acc = dense.softmax_xent(logits, self.y_p, denom=self.T_total)
         if self.rank == 0:
             c_out, c_hid = self.regul_coefs  # mlpconv.py:235-243, counted once
-            W1, W2 = self.W1, self.W2
-            loss = loss + (W2.abs().sum() * (c_out * 0.5) + (W2 * W2).sum() * (c_out * 0.5)
-                           + W1.abs().sum() * (c_hid * 0.5) + (W1 * W1).sum() * (c_hid * 0.5))
+            loss = loss + dense.l1l2_penalty([self.W2, self.W1], [(c_out * 0.5, c_out * 0.5),
+                                                                   (c_hid * 0.5, c_hid * 0.5)])
         return loss, acc
 
     # -- one optimisation step -----------------------------------------------------------

@@ -169,10 +169,10 @@ class MLPCONV:
         return dense.softmax(self.l_out(h, target_indices=rows))
 
     def _penalty(self) -> torch.Tensor:
+        # l1 / l2 shares 0.5 of each layer's regul_coef, output layer first (mlpconv.py:235-243)
         c_out, c_hid = self.regul_coefs
-        W1, W2 = self.l_hid1.W, self.l_out.W
-        return (W2.abs().sum() * (c_out * 0.5) + (W2 * W2).sum() * (c_out * 0.5)
-                + W1.abs().sum() * (c_hid * 0.5) + (W1 * W1).sum() * (c_hid * 0.5))
+        return dense.l1l2_penalty([self.l_out.W, self.l_hid1.W],
+                                  [(c_out * 0.5, c_out * 0.5), (c_hid * 0.5, c_hid * 0.5)])
 
     def _loss_acc(self, rows: gs.RowSelection, y: torch.Tensor, penalty: bool = True):
         """categorical_crossentropy(softmax(logits), y).mean() (+ penalty) and the argmax

@@ -213,6 +213,22 @@ gcg_status gcg_adam_step_f32(int64_t n, float* p, const float* g, float* m, floa
                              gcg_stream_t stream);
 
 /*
+ * The weight penalty of the MLPCONV loss (mlpconv.py:235-243: lasagne.regularization l1 =
+ * sum|W|, l2 = sum W^2, scaled by regul_coef * share) for one float32 weight of n elements:
+ *   *out = ((acc_in ? *acc_in : 0) + l1 * sum|W|) + l2 * sum W^2
+ * acc_in (nullable, may alias out) chains the weights of one loss in order. Deterministic
+ * (fixed grid, partials added in order); workspace >= GCG_L1L2_WORKSPACE_BYTES device bytes.
+ * gcg_l1l2_grad_f32 writes its gradient dW = s * (l1 * sgn(W) + 2 * l2 * W), sgn(0) = 0 (Theano's
+ * grad of abs), s = *scale_dev (the upstream gradient, a device scalar) or 1 when NULL.
+ */
+#define GCG_L1L2_WORKSPACE_BYTES 2048
+gcg_status gcg_l1l2_penalty_f32(int64_t n, const float* W, float l1, float l2,
+                                const float* acc_in, float* out, void* workspace,
+                                size_t workspace_bytes, gcg_stream_t stream);
+gcg_status gcg_l1l2_grad_f32(int64_t n, const float* W, float l1, float l2,
+                             const float* scale_dev, float* dW, gcg_stream_t stream);
+
+/*
  * CSR transpose on the device (CSR(X^T) for the X^T . dZ1 gradient of
  * mlpconv.py:71). Output is sorted by (row, col) with stable order for equal
  * entries. out_indptr int32[n_cols+1], out_indices int32[nnz], out_vals f32[nnz].

@@ -327,3 +327,26 @@ def test_matmul_autograd_on_nt_kernels(cuda):
         Wt.mul_(2.0)
     C2 = dense.matmul(At.detach(), Wt, bt)
     _check_gemm(C2.detach().cpu().numpy(), A, 2 * W, bias=b)
+
+
+def test_l1l2_penalty_vs_float64(cuda):
+    """MLPCONV's weight penalty (mlpconv.py:235-243) on the HIP reduction + gradient kernels:
+    value within 1e-6 relative of float64, deterministic (bitwise equal across calls), gradient
+    s * (l1 sgn(W) + 2 l2 W) with sgn(0) = 0 and the upstream gradient s applied."""
+    W2 = _rand((300, 129), 30, 0.05)
+    W1 = _rand((1000, 300), 31, 0.05)
+    W1[0, :7] = 0.0  # Theano's grad of abs is 0 at 0
+    coefs = [(2.5e-5, 2.5e-5), (1e-4, 3e-5)]
+    Ws = [torch.nn.Parameter(torch.from_numpy(W).to(cuda)) for W in (W2, W1)]
+    pen = dense.l1l2_penalty(Ws, coefs)
+    ref = sum(l1 * np.abs(W.astype(np.float64)).sum() + l2 * (W.astype(np.float64) ** 2).sum()
+              for W, (l1, l2) in zip((W2, W1), coefs))
+    assert abs(float(pen) - ref) <= 1e-6 * ref
+    assert float(dense.l1l2_penalty(Ws, coefs)) == float(pen)
+    (pen * 3.0).backward()
+    for W, Wt, (l1, l2) in zip((W2, W1), Ws, coefs):
+        g64 = 3.0 * (l1 * np.sign(W.astype(np.float64)) + 2 * l2 * W.astype(np.float64))
+        assert np.abs(Wt.grad.cpu().numpy() - g64).max() <= 1e-6 * np.abs(g64).max()
+    assert (Ws[1].grad[0, :7] == 0).all()
+    with torch.no_grad():
+        assert float(dense.l1l2_penalty([Ws[0]], coefs[:1])) > 0
