@@ -75,6 +75,11 @@ SIGNATURES = {
                                                C.c_float, _p, _p, _i64, _p, _p, _p]),
     "gcg_softmax_xent_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, C.c_float, _p, _p, _i64, _p,
                                        _p, _p]),
+    "gcg_project_softmax_xent_weighted_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p,
+                                                        _p, C.c_float, _p, _p, _i64, _p, _p, _p,
+                                                        _p]),
+    "gcg_softmax_xent_weighted_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, C.c_float, _p, _p, _i64,
+                                                _p, _p, _p, _p]),
     "gcg_gemm_tn_f32_workspace_bytes": (C.c_int, [_i64, _i64, _i64, _psz]),
     "gcg_gemm_tn_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p,
                                   C.c_size_t, _p]),

@@ -72,7 +72,8 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
-    float* __restrict__ loss_rows, float* __restrict__ correct_rows) {
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows,
+    const float* __restrict__ row_w) {
   constexpr int NT = 64 * WR * WC;  // threads per workgroup (4 or 8 waves)
   static_assert(WR * WC == 4 || WR * WC == 8, "4 or 8 waves per workgroup");
   constexpr int BM = 16 * RT * WR;
@@ -87,6 +88,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   // at the start so the epilogue reads them from LDS instead of waiting on global loads
   __shared__ float sbias[EPI == 1 ? BN : 1];
   __shared__ int slab[EPI == 1 ? BM : 1];
+  __shared__ float srw[EPI == 1 ? BM : 1];  // row weights (target multiplicities), 1 if none
 
   const int tid = threadIdx.x;
   const int lane = tid & 63;
@@ -219,6 +221,7 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
       // -1: no label; a label outside [0, N) becomes -2: NaN loss, no hit, no onehot
       if (labels != nullptr && (y < 0 || y >= N)) y = -2;
       slab[r] = y;
+      srw[r] = (row_w != nullptr && row < M) ? row_w[row] : 1.f;
     }
     // (issued beside the first A chunk's loads; visible after the barrier below)
   }
@@ -333,7 +336,8 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, int act, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
-    float* __restrict__ loss_rows, float* __restrict__ correct_rows) {
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows,
+    const float* __restrict__ row_w) {
   constexpr int RT = 1, WR = 4;
   constexpr int NT = 64 * WR * WC;
   constexpr int BM = 16 * RT * WR;  // 64
@@ -547,7 +551,8 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
   const float* scale_dev = nullptr;
   float* loss_rows = nullptr;
   float* correct_rows = nullptr;
-  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows;
+  const float* row_w = nullptr;
+  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows; (void)row_w;
   constexpr int NT = Cfg::NT, BM = Cfg::BM, BN = Cfg::BN, STAGE = Cfg::STAGE;
   constexpr int SL = Cfg::SL, RPI = Cfg::RPI;
   __shared__ __attribute__((aligned(16))) float smem[Cfg::FLOATS];
@@ -721,10 +726,12 @@ template <int NV>
 __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
     int M, int N, const float* __restrict__ L, int64_t ldl, const int32_t* __restrict__ labels,
     float scale, const float* __restrict__ scale_dev, float* O, int64_t ldo,
-    float* __restrict__ loss_rows, float* __restrict__ correct_rows, int vec) {
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows,
+    const float* __restrict__ row_w, int vec) {
   const int lane = threadIdx.x & 63;
   const int64_t row = static_cast<int64_t>(blockIdx.x) * 4 + (threadIdx.x >> 6);
   if (row >= M) return;
+  const float w = row_w != nullptr ? row_w[row] : 1.f;  // target multiplicity (1 if none)
   const float* lrow = L + row * ldl;
   f4 v[NV];
   float m = kNegInf;
@@ -760,11 +767,12 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
   x = reduce16_sum<64>(x);
   a = reduce16_min<64>(a);
   if (labels != nullptr && lane == 0) {
-    loss_rows[row] = bad_y ? std::numeric_limits<float>::quiet_NaN() : (m + logf(s)) - x;
-    if (correct_rows) correct_rows[row] = (!bad_y && a == y) ? 1.f : 0.f;
+    loss_rows[row] = bad_y ? std::numeric_limits<float>::quiet_NaN() : w * ((m + logf(s)) - x);
+    if (correct_rows) correct_rows[row] = (!bad_y && a == y) ? w : 0.f;
   }
   if (O == nullptr) return;  // loss / accuracy only
   if (scale_dev != nullptr) scale *= *scale_dev;
+  if (labels != nullptr) scale *= w;
   const float inv = 1.0f / s;
   float* orow = O + row * ldo;
 #pragma unroll
@@ -1011,12 +1019,12 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
                        const float* A, int64_t lda, const float* B, int64_t ldb,
                        const float* bias, int act, float* C, int64_t ldc, const int32_t* labels,
                        float scale, const float* scale_dev, float* loss_rows,
-                       float* correct_rows) {
+                       float* correct_rows, const float* row_w) {
 #define GCG_GEMM_BL_CASE(g, wc)                                                              \
   if (s.BL && s.G == g && s.WC == wc) {                                                      \
     hipLaunchKernelGGL((gemm_bl_kernel<g, wc, EPI>), grid, dim3(256 * (wc)), 0, st, M, N, K, A, \
                        lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
-                       correct_rows);                                                         \
+                       correct_rows, row_w);                                                  \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
@@ -1033,7 +1041,7 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
     hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI, pf>), grid, dim3(64 * (wr) * (wc)), 0, \
                        st, M, N, K, A,                                                       \
                        lda, B, ldb, bias, act, C, ldc, labels, scale, scale_dev, loss_rows,   \
-                       correct_rows);                                                         \
+                       correct_rows, row_w);                                                  \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
@@ -1126,7 +1134,8 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
                        const float* A, int64_t lda, const float* B, int64_t ldb,
                        const float* bias, int act, float* C, int64_t ldc,
                        const int32_t* labels, float scale, const float* scale_dev,
-                       float* loss_rows, float* correct_rows, gcg_stream_t stream) {
+                       float* loss_rows, float* correct_rows, const float* row_w,
+                       gcg_stream_t stream) {
   if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
                 static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
@@ -1144,6 +1153,8 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
     return s;
   if (labels != nullptr && loss_rows == nullptr)
     return fail(GCG_ERR_INVALID_ARG, "%s: labels given without loss_rows", fn);
+  if (row_w != nullptr && !aligned(row_w, 4))
+    return fail(GCG_ERR_MISALIGNED, "%s: row_weight not 4-B aligned", fn);
   if (M == 0) return GCG_OK;
   const Shape sh = pick_shape(N, fused);
   dim3 grid(static_cast<unsigned>((M + sh.bm() - 1) / sh.bm()),
@@ -1152,9 +1163,9 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
   auto st = static_cast<hipStream_t>(stream);
   if (fused)
     return launch_gemm<1>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
-                          labels, scale, scale_dev, loss_rows, correct_rows);
+                          labels, scale, scale_dev, loss_rows, correct_rows, row_w);
   return launch_gemm<0>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
-                        nullptr, 0.f, nullptr, nullptr, nullptr);
+                        nullptr, 0.f, nullptr, nullptr, nullptr, nullptr);
 }
 
 // NT GEMM tile variants: (RT, G, WR, WC, S). Default BM = 256 x BN = 64, two stages,
@@ -1257,7 +1268,7 @@ gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t
                         const float* B, int64_t ldb, const float* bias, int act, float* C,
                         int64_t ldc, gcg_stream_t stream) {
   return gemm_common("gcg_gemm_f32", false, M, N, K, A, lda, B, ldb, bias, act, C, ldc, nullptr,
-                     0.f, nullptr, nullptr, nullptr, stream);
+                     0.f, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
@@ -1268,13 +1279,35 @@ gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const f
                                         gcg_stream_t stream) {
   return gemm_common("gcg_project_softmax_xent_f32", true, M, N, K, A, lda, W, ldw, bias,
                      GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows, correct_rows,
-                     stream);
+                     nullptr, stream);
+}
+
+gcg_status gcg_project_softmax_xent_weighted_f32(int64_t M, int64_t N, int64_t K,
+                                                 const float* A, int64_t lda, const float* W,
+                                                 int64_t ldw, const float* bias,
+                                                 const int32_t* labels, float scale,
+                                                 const float* scale_dev, float* out,
+                                                 int64_t ldo, float* loss_rows,
+                                                 float* correct_rows, const float* row_weight,
+                                                 gcg_stream_t stream) {
+  return gemm_common("gcg_project_softmax_xent_weighted_f32", true, M, N, K, A, lda, W, ldw,
+                     bias, GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows,
+                     correct_rows, row_weight, stream);
 }
 
 gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
                                 const int32_t* labels, float scale, const float* scale_dev,
                                 float* out, int64_t ldo, float* loss_rows, float* correct_rows,
                                 gcg_stream_t stream) {
+  return gcg_softmax_xent_weighted_f32(M, N, logits, ldl, labels, scale, scale_dev, out, ldo,
+                                       loss_rows, correct_rows, nullptr, stream);
+}
+
+gcg_status gcg_softmax_xent_weighted_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
+                                         const int32_t* labels, float scale,
+                                         const float* scale_dev, float* out, int64_t ldo,
+                                         float* loss_rows, float* correct_rows,
+                                         const float* row_weight, gcg_stream_t stream) {
   const char* fn = "gcg_softmax_xent_f32";
   if (M < 0 || N <= 0 || M > INT32_MAX || N > 4096)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld (N <= 4096)", fn,
@@ -1296,7 +1329,7 @@ gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64
   if (nv <= v) {                                                                             \
     hipLaunchKernelGGL(softmax_xent_rows_kernel<v>, grid, dim3(256), 0, st, int(M), int(N), \
                        logits, ldl, labels, scale, scale_dev, out, ldo, loss_rows,          \
-                       correct_rows, vec);                                                   \
+                       correct_rows, row_weight, vec);                                       \
     GCG_HIP_CHECK(hipGetLastError());                                                        \
     return GCG_OK;                                                                           \
   }

@@ -326,7 +326,11 @@ class Projection:
         Wa, slot = _weight_on_side_stream(W)
         return _MatMul.apply(A, Wa, b, slot, self)
 
-    def softmax_xent(self, P, W, b, labels, denom: Optional[int] = None):
+    def softmax_xent(self, P, W, b, labels, denom: Optional[int] = None,
+                     row_weight: Optional[torch.Tensor] = None):
+        """row_weight: optional float32 [M] multiplicity of each row (distinct targets of a
+        list drawn with replacement); denom is then the length of the full list."""
+        row_weight = _row_weight(row_weight, P.shape[0])
         if not torch.is_grad_enabled():  # evaluation: loss and hits only, no gradient buffer
             P = _aligned_operand(P, "P")
             M = P.shape[0]
@@ -334,10 +338,11 @@ class Projection:
             y = _labels_i32(labels, M, W.shape[1])
             loss_rows = torch.empty(M, dtype=torch.float32, device=P.device)
             correct = torch.empty(M, dtype=torch.float32, device=P.device)
-            _fused(P, self.fwd.get(W, False), b, y, 1.0, None, None, loss_rows, correct)
+            _fused(P, self.fwd.get(W, False), b, y, 1.0, None, None, loss_rows, correct,
+                   row_weight)
             return loss_rows.sum() / D, correct.sum() / D
         Wa, slot = _weight_on_side_stream(W)
-        return _ProjectXent.apply(P, Wa, b, labels, self, denom, slot)
+        return _ProjectXent.apply(P, Wa, b, labels, self, denom, slot, row_weight)
 
     def probabilities(self, P, W, b) -> torch.Tensor:
         """softmax(P . W + b) rows (predict_proba) in one fused launch."""
@@ -359,7 +364,16 @@ def _labels_i32(labels: torch.Tensor, M: int, N: int) -> torch.Tensor:
     return labels.to(torch.int32).contiguous()
 
 
-def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct):
+def _row_weight(w: Optional[torch.Tensor], M: int) -> Optional[torch.Tensor]:
+    if w is None:
+        return None
+    _require_cuda(w, "row_weight")
+    if w.numel() != M:
+        raise ValueError(f"row_weight has {w.numel()} entries for {M} rows")
+    return w.detach().to(torch.float32).contiguous()
+
+
+def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weight=None):
     P = _aligned_operand(P, "P")
     M, K = P.shape
     N = Wp.shape[1]
@@ -373,10 +387,10 @@ def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct):
     if M == 0:
         return
     with torch.cuda.device(P.device):
-        call("gcg_project_softmax_xent_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp), Wp.stride(0),
-             _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
+        call("gcg_project_softmax_xent_weighted_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp),
+             Wp.stride(0), _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
              _ld(out) if out is not None else 0, _ptr(loss_rows), _ptr(correct),
-             _stream_handle(P.device))
+             _ptr(row_weight), _stream_handle(P.device))
 
 
 class _ProjectXent(torch.autograd.Function):
@@ -387,7 +401,8 @@ class _ProjectXent(torch.autograd.Function):
     dP = G . (g W)^T (hipBLASLt), dW = g P^T . G (split-K MFMA gemm_tn), db = g colsum(G)."""
 
     @staticmethod
-    def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None, slot=None):
+    def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None, slot=None,
+                row_weight=None):
         P = _aligned_operand(P, "P")
         M, N = P.shape[0], W.shape[1]
         D = float(max(M if denom is None else denom, 1))  # rows the mean is over (all ranks)
@@ -396,7 +411,7 @@ class _ProjectXent(torch.autograd.Function):
         G = empty_dense(M, N, P.device) if need_grad else None
         loss_rows = torch.empty(M, dtype=torch.float32, device=P.device)
         correct = torch.empty(M, dtype=torch.float32, device=P.device)
-        _fused(P, proj.fwd.get(W, False), b, y, 1.0 / D, None, G, loss_rows, correct)
+        _fused(P, proj.fwd.get(W, False), b, y, 1.0 / D, None, G, loss_rows, correct, row_weight)
         ctx.save_for_backward(P, W, G)
         ctx.proj = proj
         ctx.slot = slot
@@ -424,19 +439,19 @@ class _ProjectXent(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # dP = G . (g W)^T on the NT GEMM: Bt = g W, a scaled padded copy of W
             gP = gemm_nt(G, ctx.proj.bwd.get(W, False, scale=g))
-        return gP, gW, gb, None, None, None, None
+        return gP, gW, gb, None, None, None, None, None
 
 
-def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct):
+def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct, row_weight=None):
     M, N = logits.shape
     if N > ROWS_MAX_COLS:
         raise ValueError(f"softmax_xent supports up to {ROWS_MAX_COLS} classes")
     if M == 0:
         return
     with torch.cuda.device(logits.device):
-        call("gcg_softmax_xent_f32", M, N, _ptr(logits), _ld(logits), _ptr(y), float(scale),
-             _ptr(scale_dev), _ptr(out), _ld(out) if out is not None else 0, _ptr(loss_rows),
-             _ptr(correct), _stream_handle(logits.device))
+        call("gcg_softmax_xent_weighted_f32", M, N, _ptr(logits), _ld(logits), _ptr(y),
+             float(scale), _ptr(scale_dev), _ptr(out), _ld(out) if out is not None else 0,
+             _ptr(loss_rows), _ptr(correct), _ptr(row_weight), _stream_handle(logits.device))
 
 
 class _SoftmaxXent(torch.autograd.Function):
@@ -445,7 +460,7 @@ class _SoftmaxXent(torch.autograd.Function):
     g (softmax - onehot)/M in one more pass, g read on the device (graph-capturable)."""
 
     @staticmethod
-    def forward(ctx, logits, labels, denom: Optional[int] = None):
+    def forward(ctx, logits, labels, denom: Optional[int] = None, row_weight=None):
         _require_cuda(logits, "logits")
         if logits.dtype != torch.float32 or logits.dim() != 2 or \
                 (logits.shape[1] > 1 and logits.stride(1) != 1):
@@ -454,7 +469,8 @@ class _SoftmaxXent(torch.autograd.Function):
         y = _labels_i32(labels, M, N)
         loss_rows = torch.empty(M, dtype=torch.float32, device=logits.device)
         correct = torch.empty(M, dtype=torch.float32, device=logits.device)
-        _rows_call(logits, y, 1.0, None, None, loss_rows, correct)
+        _rows_call(logits, y, 1.0, None, None, loss_rows, correct, row_weight)
+        ctx.row_weight = row_weight
         ctx.save_for_backward(logits, y)
         ctx.D = float(max(M if denom is None else denom, 1))
         acc = correct.sum() / ctx.D
@@ -468,23 +484,27 @@ class _SoftmaxXent(torch.autograd.Function):
         gl = empty_dense(M, N, logits.device)
         dummy = torch.empty(M, dtype=torch.float32, device=logits.device)
         g = g_loss.reshape(1).to(torch.float32).contiguous()
-        _rows_call(logits, y, 1.0 / ctx.D, g, gl, dummy, None)
-        return gl, None, None
+        _rows_call(logits, y, 1.0 / ctx.D, g, gl, dummy, None, ctx.row_weight)
+        return gl, None, None, None
 
 
 def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None,
-                         denom: Optional[int] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+                         denom: Optional[int] = None, row_weight: Optional[torch.Tensor] = None
+                         ) -> Tuple[torch.Tensor, torch.Tensor]:
     """(mean CE loss, accuracy) of softmax(P . W + b) against labels, differentiable in P, W, b.
     denom: the row count the mean is taken over (default: these rows; the total over all
-    ranks when each rank holds a share of the targets)."""
+    ranks when each rank holds a share of the targets). row_weight: optional multiplicity of
+    each row (every row's loss, hit and gradient scaled by it)."""
     Wa, slot = _weight_on_side_stream(W)
-    return _ProjectXent.apply(P, Wa, b, labels, proj or Projection(), denom, slot)
+    return _ProjectXent.apply(P, Wa, b, labels, proj or Projection(), denom, slot,
+                              _row_weight(row_weight, P.shape[0]))
 
 
-def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int] = None
-                 ) -> Tuple[torch.Tensor, torch.Tensor]:
-    """(mean CE loss, accuracy) of existing logits, differentiable in the logits."""
-    return _SoftmaxXent.apply(logits, labels, denom)
+def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int] = None,
+                 row_weight: Optional[torch.Tensor] = None) -> Tuple[torch.Tensor, torch.Tensor]:
+    """(mean CE loss, accuracy) of existing logits, differentiable in the logits;
+    row_weight as in project_softmax_xent."""
+    return _SoftmaxXent.apply(logits, labels, denom, _row_weight(row_weight, logits.shape[0]))
 
 
 L1L2_WORKSPACE_BYTES = 2048  # GCG_L1L2_WORKSPACE_BYTES

@@ -127,6 +127,8 @@ class MLPCONV:
         self.report_k_epoch = report_k_epoch
         self.order = order  # ConvolutionDenseLayer order: reference | propagate_first | auto
         self.use_graph = use_graph  # replay each epoch's fwd+bwd+adam as one captured HIP graph
+        # repeated targets (drawn with replacement) computed once, weighted by multiplicity
+        self.distinct_targets = True
         self.history = []
 
     # -- model --------------------------------------------------------------------------
@@ -178,11 +180,20 @@ class MLPCONV:
         """categorical_crossentropy(softmax(logits), y).mean() (+ penalty) and the argmax
         accuracy (mlpconv.py:227-253), through the HIP softmax-CE kernels."""
         h = self.l_hid1(self.Xd)
+        T, w = len(rows), None
+        d = rows.distinct() if self.distinct_targets else None
+        if d is not None:
+            # targets drawn with replacement (tensormain.py:226): the output layer runs on the
+            # distinct rows, each row's loss / hit / gradient weighted by its multiplicity
+            rows, first, w = d
+            y = y.index_select(0, first)
         if self._fused_output():
             P = self.l_out.propagate(h, rows)  # (H . h)[rows], K wide
-            loss, acc = self._proj.softmax_xent(P, self.l_out.W, self.l_out.b, y)
+            loss, acc = self._proj.softmax_xent(P, self.l_out.W, self.l_out.b, y, denom=T,
+                                                row_weight=w)
         else:
-            loss, acc = dense.softmax_xent(self.l_out(h, target_indices=rows), y)
+            loss, acc = dense.softmax_xent(self.l_out(h, target_indices=rows), y, denom=T,
+                                           row_weight=w)
         if penalty:
             loss = loss + self._penalty()
         return loss, acc

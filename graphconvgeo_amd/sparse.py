@@ -89,6 +89,24 @@ class RowSelection:
     def __len__(self):
         return self.n
 
+    def distinct(self):
+        """(distinct rows as a RowSelection in increasing order, int64 device index of each
+        distinct row's first position, float32 device multiplicities) -- or None when no row
+        repeats. A target list drawn with replacement (tensormain.py:226: np.random.choice,
+        ~63 % distinct) then costs its distinct rows only: the loss and gradient of a repeated
+        target are its multiplicity times one copy's (Theano's inc_subtensor adds the copies,
+        mlpconv.py:94). Computed once per selection, on the host."""
+        if "_distinct" not in self.__dict__:
+            uniq, first, counts = np.unique(self.host, return_index=True, return_counts=True)
+            if uniq.size == self.n:
+                self._distinct = None
+            else:
+                dev = self.device_rows.device
+                self._distinct = (RowSelection(uniq, dev),
+                                  torch.from_numpy(first.astype(np.int64)).to(dev),
+                                  torch.from_numpy(counts.astype(np.float32)).to(dev))
+        return self._distinct
+
 
 # Plans released by the garbage collector are destroyed later, at the next plan creation (always
 # outside a HIP graph capture: creating a plan synchronizes), never inside __del__: a collection

@@ -358,6 +358,32 @@ gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64
                                 gcg_stream_t stream);
 
 /*
+ * Weighted forms of the two above: row i's loss, hit and gradient row are multiplied by
+ * row_weight[i] (device, nullable = all 1 -- then bitwise the unweighted calls). With the
+ * distinct targets as rows and their multiplicities as weights, one call computes the loss
+ * and gradient of a target list drawn with replacement (tensormain.py:226) over its distinct
+ * rows only: sum_i w_i loss_i = the sum over the full list, and the gradient of a distinct row
+ * is the sum of its duplicates' gradients (Theano's inc_subtensor adds them, mlpconv.py:94).
+ */
+gcg_status gcg_project_softmax_xent_weighted_f32(int64_t M, int64_t N, int64_t K,
+                                                 const float* A, int64_t lda, const float* W,
+                                                 int64_t ldw, const float* bias /*nullable*/,
+                                                 const int32_t* labels /*nullable*/, float scale,
+                                                 const float* scale_dev /*nullable*/,
+                                                 float* out /*nullable*/, int64_t ldo,
+                                                 float* loss_rows,
+                                                 float* correct_rows /*nullable*/,
+                                                 const float* row_weight /*nullable*/,
+                                                 gcg_stream_t stream);
+gcg_status gcg_softmax_xent_weighted_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
+                                         const int32_t* labels /*nullable*/, float scale,
+                                         const float* scale_dev /*nullable*/,
+                                         float* out /*nullable*/, int64_t ldo, float* loss_rows,
+                                         float* correct_rows /*nullable*/,
+                                         const float* row_weight /*nullable*/,
+                                         gcg_stream_t stream);
+
+/*
  * Weight gradient C = scale * A^T . B (Theano's grad of T.dot(h, W) w.r.t. W: h^T . gz,
  * mlpconv.py:88; P^T . G in the propagate-first order), A: R x M, B: R x N, C: M x N, the
  * reduction over R (~10^6 rows) split across workgroups on the f32 MFMA path; the per-split

@@ -156,3 +156,29 @@ def test_fused_adam_matches_elementwise_formula(cuda):
             assert float((p.detach().double() - r).abs().max()) < 1e-6, t
     # an in-place update as far as torch knows: version counters move (weight-copy caches)
     assert all(p._version >= 5 for p in ps)
+
+
+@pytest.mark.parametrize("order", ["reference", "propagate_first"])
+def test_distinct_targets_equal_full_target_list(cuda, order):
+    """Targets drawn with replacement (tensormain.py:226): the output layer on the distinct
+    rows with multiplicity weights gives the loss, accuracy and gradients of the full list
+    (within fp32 rounding: a multiplicity times one copy vs the copies added in order)."""
+    import torch
+
+    H, X, Y, train, dev, test, init = problem()
+    assert np.unique(train).size < train.size
+    res = {}
+    for distinct in (False, True):
+        clf = MLPCONV(n_epochs=0, hidden_layer_size=48, regul_coefs=(1e-5, 1e-5),
+                      init_parameters=init, device=cuda, mode="ordered", order=order)
+        clf.fit(X, train, dev, test, Y, H)
+        clf.distinct_targets = distinct
+        y = torch.as_tensor(Y[train].astype(np.int32), device=cuda)
+        loss, acc = clf._loss_acc(clf.rows["train"], y)
+        loss.backward()
+        res[distinct] = (float(loss), float(acc), [p.grad.cpu().numpy() for p in clf.params])
+    (l0, a0, g0), (l1, a1, g1) = res[False], res[True]
+    assert abs(l1 - l0) <= 1e-6 * abs(l0)
+    assert abs(a1 - a0) <= 1e-6
+    for x, z in zip(g0, g1):
+        assert np.abs(x - z).max() <= 1e-5 * max(1.0, np.abs(x).max())
