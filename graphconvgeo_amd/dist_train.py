@@ -152,6 +152,13 @@ class RowPartitionedGCN:
         pos, loc = local_targets(idx, start, stop)
         self.rows = gs.RowSelection(loc, self.device)
         self.y_p = torch.as_tensor(np.asarray(y)[idx[pos]].astype(np.int32), device=self.device)
+        # repeated local targets (drawn with replacement): the output layer runs on the
+        # distinct rows, weighted by multiplicity (MLPCONV._loss_acc does the same)
+        self.row_w = None
+        d = self.rows.distinct()
+        if d is not None:
+            self.rows, first, self.row_w = d
+            self.y_p = self.y_p.index_select(0, first)
         F = X.shape[1]
         rng = np.random.RandomState(seed)  # every rank draws the same W1, W2 (then broadcast)
         w1 = torch.as_tensor(_glorot_uniform(F, hidden, rng) if W1 is None else np.asarray(W1))
@@ -178,11 +185,13 @@ class RowPartitionedGCN:
         h = partitioned_propagate(Z1, self.part, self.b1, "relu", None, self.mode)
         if self.order == "propagate_first":
             P = partitioned_propagate(h, self.part, None, None, self.rows, self.mode)
-            loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, self.y_p, denom=self.T_total)
+            loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, self.y_p, denom=self.T_total,
+                                               row_weight=self.row_w)
         else:
             Z2 = dense.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
             logits = partitioned_propagate(Z2, self.part, self.b2, None, self.rows, self.mode)
-            loss, acc = dense.softmax_xent(logits, self.y_p, denom=self.T_total)
+            loss, acc = dense.softmax_xent(logits, self.y_p, denom=self.T_total,
+                                           row_weight=self.row_w)
         if self.rank == 0:
             c_out, c_hid = self.regul_coefs  # mlpconv.py:235-243, counted once
             loss = loss + dense.l1l2_penalty([self.W2, self.W1], [(c_out * 0.5, c_out * 0.5),
