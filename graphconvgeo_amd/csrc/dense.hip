@@ -491,10 +491,12 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
 //     also fences the buffer the next DMA overwrites: every wave finished reading it (its
 //     MFMAs consumed the reads) before arriving. All LDS is one __shared__ array (a second
 //     object makes hipcc drain the DMA queue before every ds_read).
-//   * K tail: source addresses are clamped into the row; after the last chunk lands, its
-//     elements at k >= K are zeroed in LDS (one extra barrier per tile), so garbage in the
-//     operands' padding never meets a finite factor. Rows past M / columns past N read
-//     clamped rows and are never stored.
+//   * K tail: source addresses are clamped into the row; in the step that reaches past K the
+//     fragment elements at k >= K are zeroed in registers (both operands, so garbage in the
+//     operands' padding never meets a finite factor). Until round 2 the last chunk's k >= K
+//     elements were zeroed in LDS by a 24-iteration loop per thread plus an extra barrier, once
+//     per tile (~10 % of a K = 300 tile). Rows past M / columns past N read clamped rows and
+//     are never stored.
 //   * XCD-aware order (MI355X_MICROARCH.md: workgroup b runs on XCD b % 8): workgroup b takes
 //     logical tile remap(b), each XCD walking one contiguous range of tiles in row-block-major
 //     order, so the N / BN column tiles of a row block share one XCD's L2 copy of its A rows.
@@ -523,11 +525,12 @@ struct NtCfg {
   static constexpr int PER_WAVE = NGLDS / NW;     // (exact when S >= 3)
   static constexpr int FLOATS = S * STAGE;
   static constexpr int LDS_BYTES = FLOATS * 4;
-  static constexpr int OCC = (2 * LDS_BYTES <= 160 * 1024) ? 2 : 1;
+  static constexpr int OCC_LDS = (160 * 1024) / LDS_BYTES;  // workgroups per CU the LDS allows
+  static constexpr int OCC = OCC_LDS < 1 ? 1 : (OCC_LDS > 4 ? 4 : OCC_LDS);
   static_assert(KC == 16 || KC == 32, "4- or 8-slot image rows");
   static_assert(ROWS % RPI == 0, "whole DMA instructions per stage");
   static_assert(S == 2 || NGLDS % NW == 0, "S >= 3 needs the same DMA count on every wave");
-  static_assert(S >= 2 && S <= 4, "2..4 stages");
+  static_assert(S >= 2 && S <= 6, "2..6 stages");
 };
 
 // Swizzle key of image row r (see above). 4-slot rows: pi((r >> 2) & 3), pi = {0, 2, 3, 1},
@@ -655,6 +658,20 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[t][g][e] = mfma4(af[t][ss], bf[g][e][ss], acc[t][g][e]);
   };
+  // zero the elements of a step's fragments at k >= K: lane (j, q) holds k = kb + 4q + e
+  auto mask_step = [&](f4 (&af)[RT], f4 (&bf)[G][4], int kb) {
+    const int lim = K - kb - 4 * q;  // elements e < lim are inside K
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bool in = e < lim;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) af[t][e] = in ? af[t][e] : 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e2 = 0; e2 < 4; ++e2) bf[g][e2][e] = in ? bf[g][e2][e] : 0.f;
+    }
+  };
   auto read_step = [&](const float* stage, int h, f4 (&af)[RT], f4 (&bf)[G][4]) {
 #pragma unroll
     for (int t = 0; t < RT; ++t) af[t] = frag(stage, arow0 + 16 * t, 4 * h + q);
@@ -673,8 +690,7 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
       if (c + S - 2 < n_chunks) {
-        if constexpr (S == 3) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(Cfg::PER_WAVE) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" :: "n"(2 * Cfg::PER_WAVE) : "memory");
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * Cfg::PER_WAVE) : "memory");
       } else {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
@@ -682,35 +698,34 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     lds_barrier();
     const float* stage = smem + (c % S) * STAGE;
     const int kc0 = c * KC;
-    if (kc0 + KC > K) {
-      // last chunk: zero the k >= K elements of every image row (both operands)
-      float* st = smem + (c % S) * STAGE;
-      for (int idx = tid; idx < Cfg::ROWS * KC; idx += NT) {
-        const int r = idx / KC, kk = idx % KC;
-        if (kc0 + kk >= K) st[r * KC + 4 * ((kk >> 2) ^ nt_key<SL>(r)) + (kk & 3)] = 0.f;
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      lds_barrier();
-    }
     if (c + S - 1 < n_chunks) issue(c + S - 1);
+    // K tail: a step reaching past K has its k >= K fragment elements zeroed in registers
+    // (wave-uniform branch, last chunk only); the LDS there holds clamped re-reads / padding
     if constexpr (KC == 16) {
       f4 af[RT], bf[G][4];
       read_step(stage, 0, af, bf);
+      if (kc0 + 16 > K) mask_step(af, bf, kc0);
       mfma_step(af, bf);
     } else if constexpr (PF) {
       // both 16-deep steps' fragments first: the second step's LDS reads are in flight
-      // during the first step's MFMAs (counted lgkmcnt waits); past K the LDS holds zeros
+      // during the first step's MFMAs (counted lgkmcnt waits)
       f4 af0[RT], bf0[G][4], af1[RT], bf1[G][4];
       read_step(stage, 0, af0, bf0);
       read_step(stage, 1, af1, bf1);
+      if (kc0 + 16 > K) mask_step(af0, bf0, kc0);
       mfma_step(af0, bf0);
-      if (kc0 + 16 < K) mfma_step(af1, bf1);
+      if (kc0 + 16 < K) {
+        if (kc0 + 32 > K) mask_step(af1, bf1, kc0 + 16);
+        mfma_step(af1, bf1);
+      }
     } else {
       f4 af[RT], bf[G][4];
       read_step(stage, 0, af, bf);
+      if (kc0 + 16 > K) mask_step(af, bf, kc0);
       mfma_step(af, bf);
       if (kc0 + 16 < K) {
         read_step(stage, 1, af, bf);
+        if (kc0 + 32 > K) mask_step(af, bf, kc0 + 16);
         mfma_step(af, bf);
       }
     }
@@ -1183,8 +1198,14 @@ struct NtShape {
 // BM = 128 x BN = 64 with 48-72 KB of LDS runs 2-3 workgroups per CU: one workgroup's
 // barrier, DMA wait and epilogue overlap the others' MFMAs. A deeper ring pays off on the
 // longer K loop (K = 930).
+// Round 2, later (K-tail zeroing moved to registers, occupancy hint from the LDS size):
+// 16-deep chunks in a 4-stage ring (2,1,4,1,4,KC=16): 48 KB, 3 workgroups per CU, three
+// chunks of DMA in flight: 118.0 / 118.0 / 114.4 / 111.2 on the four shapes above against
+// 108.6 / 113.3 / 112.2 / 109.9 for the 32-deep defaults (one box, mean of 10); 5-6 stages
+// (2 workgroups per CU) 104-113; 256 x 64 116 / 117.5; 128 x 128 91-115; 64 x 64 106-111.
 NtShape pick_nt_shape(int64_t K) {
-  NtShape sh = K > 512 ? NtShape{2, 1, 4, 1, 3, 1} : NtShape{2, 1, 4, 1, 2, 1};
+  (void)K;
+  NtShape sh{2, 1, 4, 1, 4, 0, 16};
   if (const char* v = std::getenv("GCG_NT_CFG")) {
     int a = 0, b = 0, c = 0, d = 0, e = 0, f = 0, kc = 32;
     const int n = std::sscanf(v, "%d,%d,%d,%d,%d,%d,%d", &a, &b, &c, &d, &e, &f, &kc);
@@ -1234,8 +1255,19 @@ gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
   GCG_NT_CASE(2, 1, 2, 2, 2, 0)
   GCG_NT_CASE(4, 1, 4, 1, 2, 0)
 #undef GCG_NT_CASE
-  if (sh.KC == 16 && sh.RT == 2 && sh.G == 1 && sh.WR == 4 && sh.WC == 1 && sh.S == 3)
-    return launch_nt_t<2, 1, 4, 1, 3, 0, 16>(a, st);
+#define GCG_NT16_CASE(rt_, g_, s_)                                                              \
+  if (sh.KC == 16 && sh.RT == rt_ && sh.G == g_ && sh.WR == 4 && sh.WC == 1 && sh.S == s_)      \
+    return launch_nt_t<rt_, g_, 4, 1, s_, 0, 16>(a, st);
+  GCG_NT16_CASE(2, 1, 2)
+  GCG_NT16_CASE(2, 1, 3)
+  GCG_NT16_CASE(2, 1, 4)
+  GCG_NT16_CASE(2, 1, 5)
+  GCG_NT16_CASE(2, 1, 6)
+  GCG_NT16_CASE(4, 1, 4)
+  GCG_NT16_CASE(2, 2, 4)
+  GCG_NT16_CASE(1, 1, 4)
+  GCG_NT16_CASE(1, 1, 6)
+#undef GCG_NT16_CASE
   return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: no tile RT=%d G=%d WR=%d WC=%d S=%d PF=%d KC=%d",
               sh.RT, sh.G, sh.WR, sh.WC, sh.S, sh.PF, sh.KC);
 }

@@ -283,7 +283,10 @@ def test_gemm_nt_vs_float64(cuda, M, K, N):
 
 @pytest.mark.parametrize("cfg", ["2,1,4,1,2,0", "2,1,4,1,2,1", "2,1,4,1,3,0", "2,1,4,1,3,1",
                                  "1,1,4,1,2,0", "1,1,4,1,3,0", "3,1,4,1,2,0", "2,2,4,1,2,0",
-                                 "2,1,2,2,2,0", "4,1,4,1,2,0", "2,1,4,1,3,0,16"])
+                                 "2,1,2,2,2,0", "4,1,4,1,2,0", "2,1,4,1,2,0,16",
+                                 "2,1,4,1,3,0,16", "2,1,4,1,4,0,16", "2,1,4,1,5,0,16",
+                                 "2,1,4,1,6,0,16", "4,1,4,1,4,0,16", "2,2,4,1,4,0,16",
+                                 "1,1,4,1,4,0,16", "1,1,4,1,6,0,16"])
 def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
     """Every instantiated tile (GCG_NT_CFG experiment knob) on ragged M / N / K, bias + relu."""
     monkeypatch.setenv("GCG_NT_CFG", cfg)
@@ -295,7 +298,7 @@ def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
 
 
 def test_gemm_nt_padding_never_leaks(cuda):
-    """The k tail is zeroed in LDS: NaN in the operands' padding columns (k >= K, inside
+    """The k tail is zeroed in the fragments: NaN in the operands' padding columns (k >= K, inside
     the row stride) and in rows past M / N must not reach C."""
     M, K, N = 200, 298, 70
     A, B = _rand((M, K), 16), _rand((K, N), 17)
@@ -350,3 +353,44 @@ def test_l1l2_penalty_vs_float64(cuda):
     assert (Ws[1].grad[0, :7] == 0).all()
     with torch.no_grad():
         assert float(dense.l1l2_penalty([Ws[0]], coefs[:1])) > 0
+
+
+@pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (40, 50, 300)])
+def test_weighted_softmax_xent_vs_float64(cuda, M, K, N):
+    """Row weights (target multiplicities, gcg_*_softmax_xent_weighted_f32): row i's loss, hit
+    and gradient row times w_i, in the fused layer (train and evaluation forms) and the row
+    kernel; all-ones weights are bitwise the unweighted kernels."""
+    P, W, b = _rand((M, K), 41, 0.3), _rand((K, N), 42, 0.3), _rand((N,), 43)
+    y = np.random.default_rng(44).integers(0, N, M).astype(np.int32)
+    w = np.random.default_rng(45).integers(1, 5, M).astype(np.float32)
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt, wt = torch.from_numpy(y).to(cuda), torch.from_numpy(w).to(cuda)
+    Wp = dense.Projection().fwd.get(Wt, False)
+    T = float(w.sum())
+    logits64 = P.astype(np.float64) @ W.astype(np.float64) + b
+    _P64, loss64, hits64, G64 = O.softmax_xent_f64(logits64, y, scale=1.0 / T)
+    G = empty_dense(M, N, cuda)
+    loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+    dense._fused(Pt, Wp, bt, yt, 1.0 / T, None, G, loss, hits, wt)
+    assert np.abs(loss.cpu().numpy() - w * loss64).max() < 1e-5 * w.max()
+    assert np.abs(G.cpu().numpy() - w[:, None] * G64).max() < 1e-5 * w.max() / T + 1e-7
+    srt = np.sort(logits64, axis=1)
+    clear = (srt[:, -1] - srt[:, -2]) > 1e-4
+    assert np.array_equal(hits.cpu().numpy()[clear], (w * hits64)[clear])
+    loss_e = torch.empty(M, device=cuda)
+    dense._fused(Pt, Wp, bt, yt, 1.0, None, None, loss_e, None, wt)  # evaluation form
+    assert torch.equal(loss_e, loss)
+    # all-ones weights: bitwise the unweighted kernel
+    G1, l1 = empty_dense(M, N, cuda), torch.empty(M, device=cuda)
+    G0, l0 = empty_dense(M, N, cuda), torch.empty(M, device=cuda)
+    dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G1, l1, None, torch.ones(M, device=cuda))
+    dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G0, l0, None)
+    assert torch.equal(G1, G0) and torch.equal(l1, l0)
+    # the row kernel on the logits: loss / accuracy over the weighted list and its gradient
+    L = torch.from_numpy(logits64.astype(np.float32)).to(cuda).requires_grad_()
+    lw, aw = dense.softmax_xent(L, yt, denom=int(T), row_weight=wt)
+    lw.backward()
+    L64 = L.detach().cpu().numpy().astype(np.float64)
+    _P, lr64, hr64, Gr64 = O.softmax_xent_f64(L64, y, scale=1.0 / T)
+    assert abs(float(lw) - (w * lr64).sum() / T) < 1e-5 * max(1.0, abs(float(lw)))
+    assert np.abs(L.grad.cpu().numpy() - w[:, None] * Gr64).max() < 1e-5 * w.max() / T + 1e-7
