@@ -289,6 +289,8 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
     t_gen = time.perf_counter() - t0
     out = {"config": cfg.name, "nodes": n, "edges": cfg.n_edges, "nnz_H": H.nnz, "nnz_X": X.nnz,
            "F": cfg.n_features, "K": K, "C": C, "train_rows": int(train.size),
+           # the output layer runs on the distinct targets, weighted by multiplicity
+           "train_rows_distinct": int(np.unique(train).size),
            "data": "synthetic", "data_gen_s": round(t_gen, 1), "steps": steps, "warmup": warmup}
     clf = None
     for order, graph in (("reference", False), ("propagate_first", False),
