@@ -1202,7 +1202,9 @@ struct NtShape {
 // 16-deep chunks in a 4-stage ring (2,1,4,1,4,KC=16): 48 KB, 3 workgroups per CU, three
 // chunks of DMA in flight: 118.0 / 118.0 / 114.4 / 111.2 on the four shapes above against
 // 108.6 / 113.3 / 112.2 / 109.9 for the 32-deep defaults (one box, mean of 10); 5-6 stages
-// (2 workgroups per CU) 104-113; 256 x 64 116 / 117.5; 128 x 128 91-115; 64 x 64 106-111.
+// (2 workgroups per CU) 104-113; 256 x 64 116 / 117.5; 128 x 128 91-115; 64 x 64 106-111;
+// 128 x 128 with 8 waves 115.0 / 101.2 / 118.9 / 95.9, 192 x 64 114.1 / 117.3 / 112.0 / 109.6
+// against 112.8 / 116.3 / 113.5 / 109.0 for the default on that box (not kept).
 NtShape pick_nt_shape(int64_t K) {
   (void)K;
   NtShape sh{2, 1, 4, 1, 4, 0, 16};
