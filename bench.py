@@ -186,7 +186,7 @@ def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev) -> dict:
     H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
     A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
     g = torch.Generator(device=dev).manual_seed(SEED + 11)
-    Z = torch.randn((H.shape[0], K), generator=g, device=dev)
+    Z = gs.empty_dense(H.shape[0], K, dev).copy_(torch.randn((H.shape[0], K), generator=g, device=dev))
     Y = gs.empty_dense(H.shape[0], K, dev)
     eff = resolve_mode(A, mode)
     gs.spmm(A, Z, out=Y, mode=eff)
@@ -252,7 +252,7 @@ def spmm_wide_variant(A, N: int, nnz: int, K: int, mode: str, reps: int, dev) ->
     """the same World SpMM at the wider hidden size K = 1500
     (tensormain.py:398), on the headline graph already resident in HBM."""
     g = torch.Generator(device=dev).manual_seed(SEED + 13)
-    Z = torch.randn((N, K), generator=g, device=dev)
+    Z = gs.empty_dense(N, K, dev).copy_(torch.randn((N, K), generator=g, device=dev))
     Y = gs.empty_dense(N, K, dev)
     gs.spmm(A, Z, out=Y, mode=mode)
     k_ms = time_events(lambda: gs.spmm(A, Z, out=Y, mode=mode), reps, dev)
@@ -360,7 +360,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=None, help="K (default: config hidden=300)")
     ap.add_argument("--mode", default="auto", choices=list(gs.MODES))
     ap.add_argument("--task-nnz", type=int, default=0)
-    ap.add_argument("--ld", type=int, default=0, help="row stride of Z/Y in floats (0 = K rounded to 4)")
+    ap.add_argument("--ld", type=int, default=0,
+                    help="row stride of Z/Y in floats (0 = the library's empty_dense layout)")
     ap.add_argument("--cpu-budget", type=float, default=6.0,
                     help="seconds of the C-port CPU extra (the scipy baseline is a fixed sample)")
     ap.add_argument("--no-variants", dest="variants", action="store_false",
@@ -412,9 +413,14 @@ def main():
     gen.manual_seed(SEED + rank)
     if world == 1 and not args.partitioned:
         A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
-        ld = max(args.ld, K)
-        Z = torch.randn((N, ld), generator=gen, device=dev, dtype=torch.float32)[:, :K]
-        Y = gs.empty_dense(N, K, dev) if args.ld == 0 else torch.empty((N, ld), device=dev)[:, :K]
+        if args.ld == 0:  # the library's row layout (sparse.row_stride: K = 300 -> 304 floats)
+            Z = gs.empty_dense(N, K, dev).copy_(
+                torch.randn((N, K), generator=gen, device=dev, dtype=torch.float32))
+            Y = gs.empty_dense(N, K, dev)
+        else:
+            ld = max(args.ld, K)
+            Z = torch.randn((N, ld), generator=gen, device=dev, dtype=torch.float32)[:, :K]
+            Y = torch.empty((N, ld), device=dev)[:, :K]
         gs.spmm(A, Z, out=Y, mode=args.mode, task_nnz=args.task_nnz)  # builds the plan
         eff = resolve_mode(A, args.mode)
         info = A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}

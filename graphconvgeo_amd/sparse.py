@@ -13,6 +13,7 @@ from __future__ import annotations
 
 import ctypes as C
 import hashlib
+import math
 from typing import Optional, Union
 
 import numpy as np
@@ -393,10 +394,36 @@ def _check_dense(Z: torch.Tensor, A: DeviceCSR):
     return Z
 
 
+def row_stride(k: int) -> int:
+    """Row stride (floats) of empty_dense's k-column rows: a multiple of 4 (16-B aligned rows,
+    dwordx4 loads / stores whatever k is), and among those the smallest whose row starts keep a
+    gathered row on the fewest 128-B lines. A k = 300 row (1200 B, at least 10 lines) at
+    stride 300 starts at 16-B steps into a line and spans 10.25 lines on average; at stride
+    304 (1216 B) every row starts 0 or 64 B into a line and spans exactly 10. Strides that are
+    a multiple of 128 B (all rows on one alignment) are skipped: 1280-B rows measured slower
+    than 1200-B ones (HBM channel interleave). Measured, World H.Z at K = 300: 6.84 -> 6.67-6.70
+    ms power-law, 9.37 -> 9.20-9.22 ms uniform (tools/gpu/ld_sweep.sh)."""
+    k4 = (k + 3) // 4 * 4
+    if k < 32 or (4 * k) % 128 == 0:
+        return k4
+    slack = 128 * (-(-4 * k // 128)) - 4 * k  # bytes a row may start into its first line
+    for ld in range(k4, k4 + 32, 4):
+        step = (4 * ld) % 128
+        if step and 128 - math.gcd(step, 128) <= slack:  # row starts: multiples of gcd
+            return ld
+    return k4
+
+
 def empty_dense(n: int, k: int, device, pad_to: int = 4) -> torch.Tensor:
-    """[n, k] float32 view of an [n, round_up(k, pad_to)] buffer: rows 16-B aligned, so
-    the kernels can use dwordx4 loads/stores whatever K is."""
-    ld = (k + pad_to - 1) // pad_to * pad_to if k > 0 else 0
+    """[n, k] float32 view of an [n, ld] buffer, ld = row_stride(k) (pad_to = 4) or k rounded
+    up to pad_to: rows 16-B aligned, so the kernels can use dwordx4 loads/stores whatever K
+    is, and gathered rows span the fewest 128-B lines."""
+    if k <= 0:
+        ld = 0
+    elif pad_to == 4:
+        ld = row_stride(k)
+    else:
+        ld = (k + pad_to - 1) // pad_to * pad_to
     buf = torch.empty((n, ld), dtype=torch.float32, device=device)
     return buf[:, :k] if ld != k else buf
 

@@ -17,7 +17,7 @@ cfg = CONFIGS["twitter-world"]
 dev = torch.device("cuda:0")
 H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
 A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
-Z = torch.randn((H.shape[0], 300), device=dev)
+Z = gs.empty_dense(H.shape[0], 300, dev).copy_(torch.randn((H.shape[0], 300), device=dev))
 Y = gs.empty_dense(H.shape[0], 300, dev)
 gs.spmm(A, Z, out=Y, mode=mode)  # plan
 torch.cuda.synchronize()
