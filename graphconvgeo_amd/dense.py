@@ -551,6 +551,8 @@ def l1l2_penalty(weights, coefs) -> torch.Tensor:
     """The MLPCONV weight penalty (mlpconv.py:235-243): sum over the weights, in the given
     order, of l1 * sum|W| + l2 * sum W^2 (l1 = regul_coef * l1_share, l2 = regul_coef *
     (1 - l1_share)), differentiable in every weight; deterministic. Device scalar."""
+    if not weights or len(weights) != len(coefs):
+        raise ValueError("l1l2_penalty needs one (l1, l2) pair per weight, at least one weight")
     for W in weights:
         _require_cuda(W, "W")
         if W.dtype != torch.float32 or not W.is_contiguous():

@@ -1,0 +1,36 @@
+"""Host-side layout rule of the dense operands (sparse.row_stride / empty_dense's row stride):
+16-B aligned rows whose gathered K floats span the fewest 128-B lines."""
+import math
+
+import pytest
+
+from graphconvgeo_amd.sparse import row_stride
+
+
+def lines(start: int, nbytes: int) -> int:
+    return (start % 128 + nbytes + 127) // 128
+
+
+@pytest.mark.parametrize("k", list(range(1, 2100, 7)) + [256, 300, 930, 1024, 1500])
+def test_row_stride_is_aligned_and_line_minimal(k):
+    ld = row_stride(k)
+    assert ld >= k and ld % 4 == 0 and ld < k + 36
+    row_b, best = 4 * k, -(-4 * k // 128)
+    starts = {(r * 4 * ld) % 128 for r in range(128)}
+    worst = max(lines(s, row_b) for s in starts)
+    k4 = (k + 3) // 4 * 4
+    if ld != k4:
+        # padding beyond round4(k) only when it buys the minimal line count on every row
+        assert worst == best
+        assert (4 * ld) % 128 != 0
+    # never worse than the plain round4(k) stride
+    base = max(lines(s, row_b) for s in {(r * 4 * k4) % 128 for r in range(128)})
+    assert worst <= base
+
+
+def test_row_stride_known_values():
+    assert row_stride(300) == 304   # 1216-B rows: 10 lines each (1200-B rows: 10.25 on average)
+    assert row_stride(930) == 932   # 3728-B rows already span the minimal 30 lines
+    assert row_stride(256) == 256   # 128-B aligned rows stay as they are
+    assert row_stride(1500) == 1500  # no stride under +32 floats reaches 47 lines on every row
+    assert math.gcd(4 * row_stride(300), 128) == 64
