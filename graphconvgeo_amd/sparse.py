@@ -57,6 +57,8 @@ def resolve_auto(A) -> str:
 HYBRID_MIN_DENSITY = 0.02
 HYBRID_MAX_COLS = 256
 HYBRID_MIN_ROWS = 65536
+# the dense-head GEMM of tmatmul runs on a side stream beside the tail gather
+TMATMUL_HEAD_SIDE_STREAM = True
 
 
 def _stream_handle(device: torch.device) -> C.c_void_p:
@@ -364,7 +366,7 @@ class DeviceCSR:
         # computed as (G^T . X_head)^T: K (300) x Fh (a multiple of 64) tiles the split-K
         # kernel with no idle waves (2.5 ms vs 3.7 ms for X_head^T . G at Twitter-World)
         main = torch.cuda.current_stream(self.device)
-        side = dense._side_stream(self.device)
+        side = dense._side_stream(self.device) if TMATMUL_HEAD_SIDE_STREAM else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
             head_t = dense.gemm_tn(G, Xh)

@@ -38,9 +38,18 @@ def main():
     ap.add_argument("--mode", default="auto")
     ap.add_argument("--order", default="reference", choices=["reference", "propagate_first", "auto"])
     ap.add_argument("--graph", action="store_true", help="replay the step as a captured HIP graph")
+    ap.add_argument("--inline-weight-grads", action="store_true",
+                    help="weight gradients on the main stream (dense.SIDE_STREAM_WEIGHT_GRADS off)")
+    ap.add_argument("--inline-head", action="store_true",
+                    help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
     args = ap.parse_args()
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
+    if args.inline_weight_grads:
+        from graphconvgeo_amd import dense
+        dense.SIDE_STREAM_WEIGHT_GRADS = False
+    if args.inline_head:
+        gs.TMATMUL_HEAD_SIDE_STREAM = False
     t0 = time.perf_counter()
     H = synthetic_graph(cfg.n_nodes, cfg.n_edges)
     X = synthetic_features(cfg.n_nodes, cfg.n_features, nnz_per_row=args.nnz_per_row)
@@ -75,18 +84,21 @@ def main():
     # SpMMs per step: X.W1, H.Z1, H.Z2 (train rows only), H.g2, H.g1, X^T.g; the layer-2
     # products are K wide instead of C under the propagate-first order.
     width2 = K if args.order == "propagate_first" or (args.order == "auto" and C > K) else C
-    # The layer-2 backward runs on (H[train])^T (sparse.rows_transpose): the targets' nonzeros
-    # only, N output rows.
-    nnz_t = int(np.diff(H.indptr)[train].sum())
+    # The layer-2 products run on the distinct targets (RowSelection.distinct) and the backward
+    # on (H[targets])^T (sparse.rows_transpose): the targets' nonzeros only, N output rows.
+    uniq = np.unique(train)
+    nnz_t = int(np.diff(H.indptr)[uniq].sum())
     sp = (spmm_bytes(n, nnzX, K) + spmm_bytes(n, nnzH, K) + spmm_bytes(n, nnz_t, width2) +
           spmm_bytes(n, nnzH, K) + spmm_bytes(cfg.n_features, nnzX, K))
-    sp_fwd_rows = spmm_bytes(len(train), nnz_t, width2)
+    sp_fwd_rows = spmm_bytes(len(uniq), nnz_t, width2)
     total = sp + sp_fwd_rows
     rec = {"metric": "GCN 2-layer fwd+bwd+adam step", "config": cfg.name, "ms_per_step": round(ms, 3),
            "nodes": n, "nnz_H": nnzH, "nnz_X": nnzX, "F": cfg.n_features, "K": K, "C": C,
-           "train_rows": len(train), "spmm_algorithmic_bytes_per_step": total,
+           "train_rows": len(train), "train_rows_distinct": int(uniq.size),
+           "spmm_algorithmic_bytes_per_step": total,
            "spmm_effective_GBps_if_all_time_in_spmm": round(total / (ms * 1e-3) / 1e9, 1),
            "mode": args.mode, "order": args.order, "hip_graph": args.graph,
+           "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
            "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
