@@ -182,3 +182,34 @@ def test_distinct_targets_equal_full_target_list(cuda, order):
     assert abs(a1 - a0) <= 1e-6
     for x, z in zip(g0, g1):
         assert np.abs(x - z).max() <= 1e-5 * max(1.0, np.abs(x).max())
+
+
+@pytest.mark.parametrize("pattern", ["one_row", "no_repeats", "heavy"])
+def test_distinct_targets_edge_cases(cuda, pattern):
+    """Distinct-target weighting at the edges: every target the same row (one distinct row of
+    multiplicity T), no repeats (the plain path), and a few rows drawn very often."""
+    import torch
+
+    H, X, Y, train, dev, test, init = problem(n=1500, e=9000)
+    n_tr = 900
+    if pattern == "one_row":
+        tgt = np.full(400, 17, dtype=np.int32)
+    elif pattern == "no_repeats":
+        tgt = np.random.default_rng(3).permutation(n_tr)[:500].astype(np.int32)
+    else:
+        tgt = np.random.default_rng(4).choice(np.arange(5), size=700).astype(np.int32)
+    res = {}
+    for distinct in (False, True):
+        clf = MLPCONV(n_epochs=0, hidden_layer_size=48, regul_coefs=(1e-5, 1e-5),
+                      init_parameters=init, device=cuda, mode="ordered", order="propagate_first")
+        clf.fit(X, tgt, dev, test, Y, H)
+        clf.distinct_targets = distinct
+        y = torch.as_tensor(Y[tgt].astype(np.int32), device=cuda)
+        loss, acc = clf._loss_acc(clf.rows["train"], y)
+        loss.backward()
+        res[distinct] = (float(loss), float(acc), [p.grad.cpu().numpy() for p in clf.params])
+    assert (clf.rows["train"].distinct() is None) == (pattern == "no_repeats")
+    (l0, a0, g0), (l1, a1, g1) = res[False], res[True]
+    assert abs(l1 - l0) <= 1e-6 * abs(l0) and abs(a1 - a0) <= 1e-6
+    for x, z in zip(g0, g1):
+        assert np.abs(x - z).max() <= 1e-5 * max(1.0, np.abs(x).max())
