@@ -36,6 +36,10 @@
 
 using namespace gcg;
 
+#ifndef GCG_SPMM_IDX_PREFETCH
+#define GCG_SPMM_IDX_PREFETCH 1
+#endif
+
 namespace {
 
 constexpr int kPanelMax = 512;  // floats per column panel
@@ -127,14 +131,36 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
   // `col` is pre-clamped for lanes past K (they re-read a column of the same row, which
   // coalesces with lane 0's line): no exec-mask branches, so hipcc can count vmcnt.
   int j = s;
+#if GCG_SPMM_IDX_PREFETCH
+  // software-pipelined (col, val) stream: the next batch's scalar loads are issued after this
+  // batch's gathers, from a clamped base (always inside the row), so they land while the
+  // gathers are in flight
+  int cn[U];
+  float vn[U];
+  if (j + U <= e) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      cn[u] = indices[j + u];
+      vn[u] = vals[j + u];
+    }
+  }
+#endif
   for (; j + U <= e; j += U) {
     int c[U];
     float v[U];
+#if GCG_SPMM_IDX_PREFETCH
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = cn[u];
+      v[u] = vn[u];
+    }
+#else
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c[u] = indices[j + u];
       v[u] = vals[j + u];
     }
+#endif
     Vec<VEC> z[U][NCH];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -143,6 +169,16 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
       for (int k = 0; k < NCH; ++k)
         z[u][k] = load_vec<VEC>(zrow + col[k]);
     }
+#if GCG_SPMM_IDX_PREFETCH
+    {
+      const int jn = min(j + U, e - U);  // in-row base; unused when no full batch follows
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        cn[u] = indices[jn + u];
+        vn[u] = vals[jn + u];
+      }
+    }
+#endif
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
