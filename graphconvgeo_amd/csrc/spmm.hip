@@ -390,7 +390,11 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   if constexpr (VEC == 4 && NCH == 2) {
     static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
     if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
-    if (inflight != 64 && a.task_nnz >= 256) return launch_rows_f<4, 2, 192>(a, n_panels, stream);
+    if (u == 24) return launch_rows_u<4, 2, 24, kWavesPerBlock>(a, n_panels, stream);
+    // planned tasks of >= 256 nnz: U = 16 since the (col, val) stream is software-pipelined
+    // (late round 2): 163 VGPRs / 3 waves per SIMD and fewer SGPR spills than U = 24 (222 VGPRs,
+    // 2 waves): World power-law 6.60 vs 6.71 ms (three alternating runs each, one box)
+    if (inflight != 64 && a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
     // plan-less, one row per wave, on a large graph (sparse.resolve_auto picks it for graphs
     // without hub rows): U = 16, 3 waves/SIMD -- Twitter-World uniform 9.35-9.36 vs 9.41-9.44 ms
     // at U = 8 (two boxes)
