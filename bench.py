@@ -59,32 +59,30 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def scipy_baseline(H, K: int, nnz_sample: int = 8_000_000, reps: int = 5) -> dict:
-    """The reference's own executor: S.dot(H, Z) (mlpconv.py:73) is scipy's `H @ Z`
-    (csr_matvecs, single-threaded whatever the host). Timed on a fixed row sample -- the
-    leading rows holding ~nnz_sample nonzeros -- against the full N x K dense operand:
-    1 warm-up, then the median of `reps` runs (time.perf_counter)."""
+def scipy_baseline(H, K: int, reps: int = 3) -> dict:
+    """The reference's own executor over the WHOLE graph: S.dot(H, Z) (mlpconv.py:73) is
+    scipy's `H @ Z` (csr_matvecs, single-threaded whatever the host), here on all nnz(H) of the
+    bench graph against the full N x K float32 operand: 1 warm-up, then the median of `reps`
+    runs (time.perf_counter) -- SURVEY.md §8d."""
     import scipy
 
-    n = H.shape[0]
-    stop = int(np.searchsorted(H.indptr, min(H.nnz, nnz_sample), side="left"))
-    blk = H[:max(stop, 1)]
     Z = np.random.default_rng(SEED + 5).standard_normal((H.shape[1], K), dtype=np.float32)
-    blk @ Z  # warm-up
+    t0 = time.perf_counter()
+    H @ Z  # warm-up
+    t_warm = time.perf_counter() - t0
     ts = []
     for _ in range(max(reps, 3)):
         t0 = time.perf_counter()
-        blk @ Z
+        H @ Z
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    return {"value": round(spmm_bytes(blk.shape[0], blk.nnz, K) / t / 1e9, 3), "unit": "GB/s",
+    return {"value": round(spmm_bytes(H.shape[0], H.nnz, K) / t / 1e9, 3), "unit": "GB/s",
             "cores": 1, "kind": "reference",
-            "edges_per_s": round(blk.nnz / t, 1),
-            "sample": f"scipy {scipy.__version__} H[:{blk.shape[0]}] @ Z ({blk.nnz} nnz x K={K}, "
-                      f"Z {H.shape[1]} x {K}), 1 warm-up + median of {len(ts)} "
+            "edges_per_s": round(H.nnz / t, 1), "seconds_per_spmm": round(t, 3),
+            "sample": f"full graph: scipy {scipy.__version__} H @ Z over all {H.shape[0]} rows "
+                      f"({H.nnz} nnz x K={K}), 1 warm-up ({t_warm:.2f} s) + median of {len(ts)} "
                       f"({', '.join(f'{x:.2f}' for x in ts)} s), single-threaded scipy "
-                      f"csr_matvecs on {cpu_model()} ({os.cpu_count()} host cpus); "
-                      f"extrapolated whole graph: {H.nnz / (blk.nnz / t):.1f} s"}
+                      f"csr_matvecs on {cpu_model()} ({os.cpu_count()} host cpus)"}
 
 
 def cpu_baseline(H, K: int, budget_s: float) -> dict:
@@ -313,23 +311,28 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
                                                           "loss": round(float(loss), 5)}
     # each SpMM of the step alone, on the last model's device operands
     A, Xd = clf.l_hid1.H, clf.Xd
+    # the output layer runs on the distinct targets (RowSelection.distinct, weighted by
+    # multiplicity), so its SpMMs are timed on those rows, as the training step runs them
     rows = clf.rows["train"]
+    if rows.distinct() is not None:
+        rows = rows.distinct()[0]
+    n_t = rows.n
     g = torch.Generator(device=dev).manual_seed(SEED + 21)
     Z1 = gs.empty_dense(n, K, dev).copy_(torch.randn((n, K), generator=g, device=dev))
-    G2 = gs.empty_dense(train.size, C, dev).copy_(torch.randn((train.size, C), generator=g, device=dev))
+    G2 = gs.empty_dense(n_t, C, dev).copy_(torch.randn((n_t, C), generator=g, device=dev))
     W1 = clf.l_hid1.W.detach()
     b1 = clf.l_hid1.b.detach()
     gate = gs.empty_gate(n, K, dev)
     At = A.rows_transpose(rows)
-    nnz_t = int(np.diff(H.indptr)[train].sum())
+    nnz_t = int(np.diff(H.indptr)[rows.host].sum())
     ops = {
         "X.W1 (mlpconv.py:71)": (lambda: gs.spmm(Xd, W1), spmm_bytes(n, X.nnz, K),
                                  "W1 (12 MB) cache-resident"),
         "rectify(H.Z1 + b1) + gate (mlpconv.py:73-77)": (
             lambda: gs.spmm(A, Z1, bias=b1, act="relu", gate=gate), spmm_bytes(n, H.nnz, K), ""),
-        "(H.Z2 + b2)[train], C wide (mlpconv.py:90-94)": (
-            lambda: gs.spmm(A, Z1[:, :C], rows=rows), spmm_bytes(train.size, nnz_t, C), ""),
-        "(H[train])^T.G2, C wide (grad of mlpconv.py:90-94)": (
+        "(H.Z2 + b2)[train distinct], C wide (mlpconv.py:90-94)": (
+            lambda: gs.spmm(A, Z1[:, :C], rows=rows), spmm_bytes(n_t, nnz_t, C), ""),
+        "(H[train distinct])^T.G2, C wide (grad of mlpconv.py:90-94)": (
             lambda: gs.spmm(At, G2), spmm_bytes(n, nnz_t, C), ""),
         "H.g1 (grad of mlpconv.py:73)": (lambda: gs.spmm(A, Z1), spmm_bytes(n, H.nnz, K), ""),
         "X^T.g (grad of mlpconv.py:71)": (lambda: Xd.tmatmul(Z1), spmm_bytes(cfg.n_features, X.nnz, K),

@@ -47,11 +47,17 @@ def source_hash() -> str:
     return h.hexdigest()[:16]
 
 
+HASH_FILE = LIB + ".hash"
+
+
 def needs_build() -> bool:
-    if not os.path.exists(LIB):
+    """True when the library is missing or was built from different sources. Decided by the
+    content hash written next to the library after a successful link (the same hash the
+    library bakes in and `_native._check_fresh` compares), never by mtime."""
+    if not os.path.exists(LIB) or not os.path.exists(HASH_FILE):
         return True
-    t = os.path.getmtime(LIB)
-    return any(os.path.getmtime(p) > t for p in (*SOURCES, *INTERNAL_HEADERS, HEADER, __file__))
+    with open(HASH_FILE) as f:
+        return f.read().strip() != source_hash()
 
 
 def build_native(force: bool = False, verbose: bool = False) -> str:
@@ -88,6 +94,9 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
         if res.returncode != 0:
             raise RuntimeError(f"link failed ({res.returncode}):\n{res.stdout}\n{res.stderr}")
         os.replace(tmp, LIB)
+        with open(HASH_FILE + ".tmp", "w") as f:
+            f.write(digest + "\n")
+        os.replace(HASH_FILE + ".tmp", HASH_FILE)
     return LIB
 
 

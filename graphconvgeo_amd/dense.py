@@ -199,8 +199,9 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
 # side stream; the consumer's backward leaves (A, G, scale) in a slot and hands the identity
 # node a placeholder; the identity node's backward computes the gradient on the side stream.
 # The engine joins the streams (event waits) where gradients cross and at the end of
-# backward() -- also inside a HIP graph capture. The slot keeps A and G alive until the
-# autograd graph is freed, after that join.
+# backward() -- also inside a HIP graph capture. A and G are marked used by the side stream
+# (record_stream) before the kernel reads them, so the caching allocator does not recycle them
+# for the main stream while it runs, whenever the autograd graph is freed.
 _SIDE_STREAMS: dict = {}
 SIDE_STREAM_WEIGHT_GRADS = True
 
@@ -233,6 +234,14 @@ class _SideWeightGrad(torch.autograd.Function):
         if ctx.slot.args is None:  # the consumer produced no weight gradient
             return None, None
         A, G, scale = ctx.slot.args
+        ctx.slot.args = None
+        # A and G were allocated on the main stream and are read here on the side stream:
+        # tell the caching allocator, so their blocks are not handed to a main-stream
+        # allocation before this kernel has finished, whenever the autograd graph lets go
+        side = torch.cuda.current_stream(A.device)
+        for t in (A, G, scale):
+            if t is not None:
+                t.record_stream(side)
         return gemm_tn(A, G, scale=scale), None
 
 
@@ -242,6 +251,7 @@ def _weight_on_side_stream(W: torch.Tensor):
             and W.is_cuda):
         return W, None
     slot = _Slot()
+    W._gcg_side_grad = True  # l1l2_penalty puts this weight's penalty node on the side stream
     with torch.cuda.stream(_side_stream(W.device)):
         Wa = _SideWeightGrad.apply(W, slot)
     return Wa, slot
@@ -511,17 +521,17 @@ L1L2_WORKSPACE_BYTES = 2048  # GCG_L1L2_WORKSPACE_BYTES
 
 
 class _L1L2Penalty(torch.autograd.Function):
-    """sum_i l1_i * sum|W_i| + l2_i * sum W_i^2, added up in the order of the weights: two
-    launches per weight forward (gcg_l1l2_penalty_f32), one per weight backward
+    """acc + sum_i l1_i * sum|W_i| + l2_i * sum W_i^2, added up in the order of the weights: one
+    launch pair per weight forward (gcg_l1l2_penalty_f32), one launch per weight backward
     (gcg_l1l2_grad_f32, the upstream gradient read on the device), instead of ~20 elementwise
-    and reduction torch kernels for the penalty and its gradient per training step."""
+    and reduction torch kernels for the penalty and its gradient per training step. `acc` (a
+    device scalar or None) is the running sum of the previous weights' node."""
 
     @staticmethod
-    def forward(ctx, coefs, *weights):
+    def forward(ctx, coefs, acc, *weights):
         dev = weights[0].device
         out = torch.empty((), dtype=torch.float32, device=dev)
         ws = torch.empty(L1L2_WORKSPACE_BYTES // 4, dtype=torch.float32, device=dev)
-        acc = None
         with torch.cuda.device(dev):
             for W, (l1, l2) in zip(weights, coefs):
                 call("gcg_l1l2_penalty_f32", W.numel(), _ptr(W), float(l1), float(l2), _ptr(acc),
@@ -533,10 +543,11 @@ class _L1L2Penalty(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, g):
+        g_acc = g if ctx.needs_input_grad[1] else None
         g = g.reshape(1).to(torch.float32).contiguous()
         grads = []
         for i, (W, (l1, l2)) in enumerate(zip(ctx.saved_tensors, ctx.coefs)):
-            if not ctx.needs_input_grad[1 + i]:
+            if not ctx.needs_input_grad[2 + i]:
                 grads.append(None)
                 continue
             dW = torch.empty_like(W)
@@ -544,20 +555,49 @@ class _L1L2Penalty(torch.autograd.Function):
                 call("gcg_l1l2_grad_f32", W.numel(), _ptr(W), float(l1), float(l2), _ptr(g),
                      _ptr(dW), _stream_handle(W.device))
             grads.append(dW)
-        return (None, *grads)
+        return (None, g_acc, *grads)
 
 
 def l1l2_penalty(weights, coefs) -> torch.Tensor:
     """The MLPCONV weight penalty (mlpconv.py:235-243): sum over the weights, in the given
     order, of l1 * sum|W| + l2 * sum W^2 (l1 = regul_coef * l1_share, l2 = regul_coef *
-    (1 - l1_share)), differentiable in every weight; deterministic. Device scalar."""
+    (1 - l1_share)), differentiable in every weight; deterministic. Device scalar.
+
+    A weight whose product gradient is computed on the side stream (_weight_on_side_stream)
+    gets its penalty node on that stream too, so every gradient reaching that weight is
+    produced on the stream its AccumulateGrad node lives on (no cross-stream accumulation);
+    consecutive weights on one stream share a node, and the running sum is chained from node
+    to node in the given order (the same kernels and the same sum as one node)."""
     if not weights or len(weights) != len(coefs):
         raise ValueError("l1l2_penalty needs one (l1, l2) pair per weight, at least one weight")
     for W in weights:
         _require_cuda(W, "W")
         if W.dtype != torch.float32 or not W.is_contiguous():
             raise TypeError("l1l2_penalty needs contiguous float32 weights")
-    return _L1L2Penalty.apply(tuple((float(a), float(b)) for a, b in coefs), *weights)
+    coefs = [(float(a), float(b)) for a, b in coefs]
+    dev = weights[0].device
+    main = torch.cuda.current_stream(dev)
+    groups = []  # [(on_side, [indices])]
+    for i, W in enumerate(weights):
+        side = bool(getattr(W, "_gcg_side_grad", False)) and torch.is_grad_enabled() \
+            and W.requires_grad
+        if groups and groups[-1][0] == side:
+            groups[-1][1].append(i)
+        else:
+            groups.append((side, [i]))
+    acc = None
+    for side, idx in groups:
+        ws = [weights[i] for i in idx]
+        cs = tuple(coefs[i] for i in idx)
+        if side:
+            s = _side_stream(dev)
+            s.wait_stream(main)
+            with torch.cuda.stream(s):
+                acc = _L1L2Penalty.apply(cs, acc, *ws)
+            main.wait_stream(s)
+        else:
+            acc = _L1L2Penalty.apply(cs, acc, *ws)
+    return acc
 
 
 def softmax(logits: torch.Tensor) -> torch.Tensor:

@@ -12,9 +12,9 @@ Reference (Lasagne `Layer` subclasses, Theano graph, host CPU):
 Here: torch modules with the same constructor arguments and `get_output_for` /
 `forward(input, target_indices=None)`. The sparse products run in the HIP kernels
 (graphconvgeo_amd.sparse.spmm) with bias + rectify + the target-row subset fused in the
-epilogue; the dense projection T.dot(h, W) is an fp32 GEMM on the f32 MFMA path (hipBLASLt
-forward, its weight gradient on the split-K MFMA kernel of csrc/dense.hip; the trainer's
-output layer is one fused MFMA kernel, graphconvgeo_amd.dense). Backward follows Theano's rules: grad of
+epilogue; the dense projection T.dot(h, W) runs on the hand-written f32 MFMA kernels of csrc/dense.hip
+(forward and input gradient on the LDS-DMA NT GEMM, the weight gradient on the split-K
+kernel; the trainer's output layer is one fused MFMA kernel, graphconvgeo_amd.dense). Backward follows Theano's rules: grad of
 S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H for the symmetric H; CSR(X^T) built once on the
 device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
 
@@ -353,6 +353,10 @@ class GCN(nn.Module):
         if Hd.symmetric is None:
             Hd.symmetric = True  # D^-1/2 (A+I) D^-1/2 of an undirected graph (tensormain.py:170-180)
         self.X = _as_device_csr(X, self.device)
+        if isinstance(rng, (int, np.integer)):
+            # one stream for both layers: W1 then W2 drawn in sequence (an int handed to each
+            # layer separately would restart the stream and make W2 a rescaled copy of W1)
+            rng = np.random.RandomState(int(rng))
         self.l_hid1 = SparseConvolutionDenseLayer(in_features, H=Hd, num_units=hidden, W=W1,
                                                   nonlinearity="rectify", device=self.device,
                                                   mode=mode, rng=rng)

@@ -51,7 +51,8 @@ def resolve_auto(A) -> str:
 
 # DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
 # the dense MFMA GEMM -- break-even is ~1.5-2 % (a gathered nonzero ~190 ps, a dense element
-# ~3-9 ps at Twitter-World, tools/exp_xtg_head.py / exp_tn_shapes.py); at most HYBRID_MAX_COLS
+# ~3-9 ps at Twitter-World, round-1 measurements; the head size re-checked in round 2 with
+# tools/exp_hybrid_cols.py); at most HYBRID_MAX_COLS
 # of them (the GEMM's cost grows faster than the gather it saves beyond), and only
 # for matrices of at least HYBRID_MIN_ROWS rows (below that everything is cache-resident).
 HYBRID_MIN_DENSITY = 0.02

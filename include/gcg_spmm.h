@@ -317,8 +317,10 @@ gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t
  * (Bt: N x K row-major, ldbt >= round4(K), ldbt % 4 == 0, 16-B aligned base; A likewise with
  * lda). The projection T.dot(h, W) (mlpconv.py:88) with Bt = W^T, and Theano's input
  * gradient g . W^T with Bt = W itself. Both operands are k-contiguous, so both go to LDS
- * through the asynchronous LDS-DMA (global_load_lds) in 32-deep chunks; the k tail is
- * zeroed in LDS, so operand padding may hold anything. Same numerics as gcg_gemm_f32.
+ * through the asynchronous LDS-DMA (global_load_lds) into a ring of k chunks (default: 16-deep
+ * chunks, 4 stages); in the 16-deep step that reaches past K the fragment elements at k >= K
+ * are zeroed in registers, so operand padding may hold anything (NaN included). Same numerics
+ * as gcg_gemm_f32.
  */
 gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                            const float* Bt, int64_t ldbt, const float* bias /*nullable*/,
