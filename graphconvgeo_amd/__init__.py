@@ -3,6 +3,7 @@
 Product modules (all compute runs in libgcg_spmm.so HIP kernels; no CPU fallback):
   sparse       DeviceCSR (H / X resident in HBM), spmm (= S.dot + fused epilogue)
   layers       GraphConvLayer, SparseConvolutionDenseLayer, ConvolutionDenseLayer, GCN
+  ops          the hot path as torch.ops.gcg.* custom ops with fake kernels (torch.compile)
   dense        output layer on the MFMA cores: f32 GEMMs, fused projection + softmax + CE
   distributed  1-D row partition of H + RCCL all-gather / halo exchange of the dense operand
   dist_train   the row-partitioned GCN training step (backward through H's symmetry)
@@ -13,5 +14,5 @@ Product modules (all compute runs in libgcg_spmm.so HIP kernels; no CPU fallback
 """
 __version__ = "0.1.0"
 
-__all__ = ["sparse", "layers", "dense", "distributed", "dist_train", "graph", "mentions",
+__all__ = ["sparse", "ops", "layers", "dense", "distributed", "dist_train", "graph", "mentions",
            "mlpconv", "synth"]

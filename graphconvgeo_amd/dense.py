@@ -29,6 +29,7 @@ import ctypes as C
 
 import torch
 
+from . import ops as _ops  # registers torch.ops.gcg.* (the compiled path)
 from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call
 from .sparse import _ptr, _require_cuda, _stream_handle, column_sum, empty_dense
 
@@ -313,6 +314,8 @@ def projection_of(W: torch.Tensor) -> "Projection":
 def matmul(A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Differentiable A . W (+ b) on the MFMA kernels (forward and input gradient: gemm_nt;
     weight gradient: gemm_tn on a side stream, overlapping the rest of the backward)."""
+    if torch.compiler.is_compiling():  # the registered op gcg::dense_matmul (ops.py)
+        return _ops.dense_matmul(A, W, b)
     proj = projection_of(W)
     Wa, slot = _weight_on_side_stream(W)
     return _MatMul.apply(A, Wa, b, slot, proj)
@@ -333,6 +336,8 @@ class Projection:
 
     def matmul(self, A: torch.Tensor, W: torch.Tensor, b: Optional[torch.Tensor] = None
                ) -> torch.Tensor:
+        if torch.compiler.is_compiling():
+            return _ops.dense_matmul(A, W, b)
         Wa, slot = _weight_on_side_stream(W)
         return _MatMul.apply(A, Wa, b, slot, self)
 
@@ -341,6 +346,8 @@ class Projection:
         """row_weight: optional float32 [M] multiplicity of each row (distinct targets of a
         list drawn with replacement); denom is then the length of the full list."""
         row_weight = _row_weight(row_weight, P.shape[0])
+        if torch.compiler.is_compiling():  # gcg::project_softmax_xent (ops.py)
+            return _ops.project_softmax_xent(P, W, b, labels, denom, row_weight)
         if not torch.is_grad_enabled():  # evaluation: loss and hits only, no gradient buffer
             P = _aligned_operand(P, "P")
             M = P.shape[0]
@@ -505,6 +512,8 @@ def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None,
     denom: the row count the mean is taken over (default: these rows; the total over all
     ranks when each rank holds a share of the targets). row_weight: optional multiplicity of
     each row (every row's loss, hit and gradient scaled by it)."""
+    if torch.compiler.is_compiling():  # gcg::project_softmax_xent (ops.py)
+        return _ops.project_softmax_xent(P, W, b, labels, denom, _row_weight(row_weight, P.shape[0]))
     Wa, slot = _weight_on_side_stream(W)
     return _ProjectXent.apply(P, Wa, b, labels, proj or Projection(), denom, slot,
                               _row_weight(row_weight, P.shape[0]))

@@ -37,6 +37,7 @@ import torch
 import torch.nn as nn
 
 from . import dense
+from . import ops as _ops  # registers torch.ops.gcg.* (the compiled path)
 from . import sparse as gs
 
 _FUSED_ACTS = {"rectify": "relu", "relu": "relu"}
@@ -86,10 +87,10 @@ def _upload_cached(cache: dict, x, device) -> gs.DeviceCSR:
     """Upload a host sparse input once and reuse it while the same object is passed
     (the reference feeds the same X to every epoch, mlpconv.py:294-295). The cache holds
     a weak reference, so a new matrix that reuses a freed object's id() is re-uploaded."""
-    import weakref
-
     if isinstance(x, gs.DeviceCSR):
         return x
+    import weakref
+
     ref = cache.get("ref")
     if ref is not None and ref() is x and cache.get("sig") == (x.shape, x.nnz):
         return cache["dev"]
@@ -167,7 +168,12 @@ def _index_csr_cached(rows: gs.RowSelection, n_rows: int):
 def csr_matmul(A: gs.DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
                act: Optional[str] = None, rows: Optional[gs.RowSelection] = None,
                mode: str = "auto") -> torch.Tensor:
-    """Differentiable S.dot(A, Z) (+ bias, rectify, row subset) through the HIP kernels."""
+    """Differentiable S.dot(A, Z) (+ bias, rectify, row subset) through the HIP kernels.
+    Under torch.compile the registered op gcg::spmm_csr (graphconvgeo_amd.ops: same kernels,
+    a fake kernel for tracing, its autograd formula made of gcg ops) stands in for the
+    autograd.Function."""
+    if torch.compiler.is_compiling():
+        return _ops.spmm_csr(A, Z, bias, act, rows, mode)
     return _CSRMatMul.apply(Z, bias, A, act, rows, mode)
 
 

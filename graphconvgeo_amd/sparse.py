@@ -13,7 +13,9 @@ from __future__ import annotations
 
 import ctypes as C
 import hashlib
+import itertools
 import math
+import weakref
 from typing import Optional, Union
 
 import numpy as np
@@ -62,6 +64,27 @@ HYBRID_MIN_ROWS = 65536
 TMATMUL_HEAD_SIDE_STREAM = True
 
 
+# Integer ids of operators and row lists, for the registered torch ops (graphconvgeo_amd.ops):
+# a custom op takes tensors and scalars only, so gcg::spmm_csr names its DeviceCSR / RowSelection
+# by the id given here at construction. Weak: the registry never keeps an operator alive.
+_OBJECTS: "weakref.WeakValueDictionary" = weakref.WeakValueDictionary()
+_NEXT_ID = itertools.count(1)
+
+
+def _register_object(obj) -> int:
+    i = next(_NEXT_ID)
+    _OBJECTS[i] = obj
+    return i
+
+
+def registered(op_id: int):
+    """The DeviceCSR / RowSelection registered under op_id (graphconvgeo_amd.ops)."""
+    try:
+        return _OBJECTS[op_id]
+    except KeyError:
+        raise KeyError(f"no live sparse operator or row list with id {op_id}") from None
+
+
 def _stream_handle(device: torch.device) -> C.c_void_p:
     return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
 
@@ -89,6 +112,7 @@ class RowSelection:
         self.n = int(host.size)
         self.key = hashlib.blake2b(host.tobytes(), digest_size=16).hexdigest() + f":{self.n}"
         self.device_rows = torch.from_numpy(host).to(device)
+        self.op_id = _register_object(self)
 
     def __len__(self):
         return self.n
@@ -192,6 +216,7 @@ class DeviceCSR:
         self.symmetric = symmetric
         self._plans = {}
         self._transpose = None
+        self.op_id = _register_object(self)
         if validate:
             self.validate()
 

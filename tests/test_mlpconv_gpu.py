@@ -213,3 +213,22 @@ def test_distinct_targets_edge_cases(cuda, pattern):
     assert abs(l1 - l0) <= 1e-6 * abs(l0) and abs(a1 - a0) <= 1e-6
     for x, z in zip(g0, g1):
         assert np.abs(x - z).max() <= 1e-5 * max(1.0, np.abs(x).max())
+
+
+@pytest.mark.parametrize("order", ["reference", "propagate_first"])
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_training_raises_no_stream_warnings(cuda, order, use_graph):
+    """The side-stream weight gradients leave no cross-stream accumulation behind: every
+    gradient reaching W2 (its product gradient and its penalty gradient) is produced on the
+    stream its AccumulateGrad node lives on, so torch's stream-mismatch warning never fires
+    (eager epochs and a captured HIP graph alike)."""
+    import warnings
+
+    H, X, Y, train, dev, test, init = problem(n=2000, e=12000, f=150, k=16, c=5)
+    with warnings.catch_warnings(record=True) as caught:
+        warnings.simplefilter("always")
+        MLPCONV(n_epochs=11, hidden_layer_size=16, regul_coefs=(1e-5, 1e-5), init_parameters=init,
+                device=cuda, report_k_epoch=5, order=order, use_graph=use_graph
+                ).fit(X, train, dev, test, Y, H)
+    msgs = [str(w.message) for w in caught if "stream" in str(w.message).lower()]
+    assert not msgs, msgs[:2]

@@ -73,3 +73,61 @@ def test_isolated_nodes_bias_gradient(cuda, mode):
     assert np.abs(contrib).max() > 100 * tol
     got_W1 = model.l_hid1.W.grad.cpu().numpy()
     assert np.abs(got_W1 - gr["W1"]).max() < 1e-5 * max(1.0, np.abs(gr["W1"]).max())
+
+
+def _gate_of(pre: np.ndarray) -> np.ndarray:
+    return (2 * (pre > 0) + (pre == 0)).astype(np.uint8)
+
+
+def test_gate_bytes_split_rows_fast(cuda):
+    """mode='fast' with a small task size: the hub rows are split into segments and the
+    spmm_fixup_kernel writes their output and gate bytes. The gate must be the sign of the
+    kernel's own pre-activation (same plan, no activation), with exact zeros in the split rows."""
+    n, k = 5000, 40
+    u, v = uniform_edges(n, 30000, seed=5)
+    hubs = np.array([0, 17, 4999])
+    hu = np.repeat(hubs, 1500)
+    hv = np.concatenate([np.random.default_rng(h).choice(np.arange(n), 1500, replace=False)
+                         for h in hubs])
+    keep = hu != hv
+    H = csr_from_edges(n, np.concatenate([u, hu[keep]]), np.concatenate([v, hv[keep]]))
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    g = torch.Generator(device=cuda).manual_seed(3)
+    Z = torch.randn((n, k), device=cuda, generator=g)
+    Z[:, :4] = 0.0  # exact-zero pre-activations in every row, the split hub rows included
+    b = torch.zeros(k, device=cuda)
+    b[4:7] = torch.tensor([1.0, -1.0, 0.0])
+    task = 256
+    plan = A.plan(None, ordered=False, task_nnz=task)
+    assert plan.info()["n_long_rows"] >= len(hubs)  # the fixup path really runs
+    pre = gs.spmm(A, Z, bias=b, mode="fast", task_nnz=task).cpu().numpy()
+    gate = gs.empty_gate(n, k, cuda)
+    Y = gs.spmm(A, Z, bias=b, act="relu", mode="fast", task_nnz=task, gate=gate)
+    assert np.array_equal(gate.cpu().numpy(), _gate_of(pre))
+    assert np.array_equal(Y.cpu().numpy(), O.relu(pre))
+    assert (gate.cpu().numpy()[hubs, :4] == 1).all()
+    # and the split rows stay within the 1e-5 bar of the float64 product
+    ref = H.astype(np.float64) @ Z.cpu().numpy().astype(np.float64) + b.cpu().numpy()
+    assert np.abs(pre - ref).max() < 1e-5
+
+
+def test_gate_bytes_rowwise_large_row_subset(cuda):
+    """The plan-less rowwise launch on >= 65536 output rows (U = 16 per wave there) with a row
+    subset: gate bytes and outputs bitwise the oracle's, exact zeros included."""
+    n, k = 70000, 24
+    u, v = uniform_edges(n, 200000, seed=9)
+    H = csr_from_edges(n, u, v)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    rows = np.random.default_rng(4).choice(n, 66000, replace=True).astype(np.int32)
+    g = torch.Generator(device=cuda).manual_seed(5)
+    Z = torch.randn((n, k), device=cuda, generator=g)
+    Z[:, :3] = 0.0
+    b = torch.zeros(k, device=cuda)
+    b[3:6] = torch.tensor([0.5, -0.5, 0.0])
+    gate = gs.empty_gate(rows.size, k, cuda)
+    sel = gs.RowSelection(rows, cuda)
+    Y = gs.spmm(A, Z, bias=b, act="relu", rows=sel, mode="rowwise", gate=gate)
+    pre = O.spmm_f32(H, Z.cpu().numpy(), bias=b.cpu().numpy())[rows]
+    assert np.array_equal(gate.cpu().numpy(), _gate_of(pre))
+    assert np.array_equal(Y.cpu().numpy(), O.relu(pre))
+    assert (gate.cpu().numpy()[:, :3] == 1).all()
