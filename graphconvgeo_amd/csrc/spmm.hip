@@ -215,13 +215,141 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
   }
 }
 
+// Barrier for LDS hand-over between the waves of a workgroup: retires this wave's LDS
+// operations only (the gathers stay in flight across it), then s_barrier.
+__device__ __forceinline__ void lds_handover_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// One long row of the bitwise 'ordered' mode, by a whole workgroup (round 3). A hub row of a
+// power-law graph on a single wave is bound by that wave's U gathers in flight (~12k nonzeros
+// take ~1.5 ms, longer than a whole 8-way row block's SpMM). Here the WPB waves gather WPB x U
+// consecutive nonzeros per batch -- WPB times the row bytes in flight -- and the storage-order
+// sum is handed from wave to wave: wave w adds its U products (nonzeros w*U .. w*U+U-1 of the
+// batch) to the running row sum in LDS, in order, then wave w+1 continues. Every addition is
+// the one the single-wave loop makes, in the same order: bitwise equal (scipy csr_matvecs).
+// A wave issues its next batch's gathers right after its own hand-over, so they fly while the
+// later waves of this batch add. LDS: one row sum (<= 512 floats).
+template <int VEC, int NCH, int U, int WPB>
+__device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
+                                         const int32_t* __restrict__ indices,
+                                         const float* __restrict__ vals,
+                                         const int32_t* __restrict__ out_rows,
+                                         const float* __restrict__ Z, int64_t ldz,
+                                         const int (&col)[NCH], const int (&gcol)[NCH],
+                                         const bool (&on)[NCH], float* __restrict__ Y,
+                                         int64_t ldy, const float* __restrict__ bias, int act,
+                                         uint8_t* __restrict__ gate, int64_t ldgate,
+                                         float* __restrict__ sacc) {
+  const int wave = uniform(static_cast<int>(threadIdx.x >> 6));
+  const int lane = threadIdx.x & (kWave - 1);
+  const int r = out_rows ? uniform(out_rows[p]) : p;
+  const int s = uniform(indptr[r]);
+  const int e = uniform(indptr[r + 1]);
+  constexpr int B = WPB * U;  // nonzeros per batch
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) sacc[(k * kWave + lane) * VEC + q] = 0.0f;
+  }
+  // (col, val) of this wave's nonzeros of a batch: one VECTOR load per wave (lane u holds
+  // nonzero u, indices clamped into the row -- coop rows are never empty), prefetched one batch
+  // ahead and moved to SGPRs with readlane when the batch is gathered. (Scalar-loaded pairs,
+  // as in accumulate_range, spill to VGPR lanes here -- 160 SGPRs -- and every spill waits for
+  // its s_load: one scalar-load latency per hand-over stage, 5.7 us per batch.)
+  int c[U];
+  float v[U];
+  Vec<VEC> z[U][NCH];
+  static_assert(U <= kWave, "one lane per nonzero of a wave's batch");
+  const int lu = min(lane, U - 1);
+  auto load_idx = [&](int j0, int& ci, float& vi) {
+    const int jj = min(j0 + lu, e - 1);
+    ci = indices[jj];
+    vi = vals[jj];
+  };
+  auto gather = [&](int ci, float vi) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = __builtin_amdgcn_readlane(ci, u);
+      v[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vi), u));
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+#pragma unroll
+      for (int k = 0; k < NCH; ++k) z[u][k] = load_vec<VEC>(zrow + gcol[k]);
+    }
+  };
+  int ci, cin;
+  float vi, vin;
+  load_idx(s + wave * U, ci, vi);
+  gather(ci, vi);
+  load_idx(s + B + wave * U, cin, vin);
+  lds_handover_barrier();
+  for (int b = s; b < e; b += B) {
+    for (int st = 0; st < WPB; ++st) {
+      if (st == wave) {
+        const int n = min(U, max(0, e - (b + wave * U)));  // this wave's nonzeros, uniform
+        Vec<VEC> acc[NCH];
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+          acc[k] = *reinterpret_cast<const Vec<VEC>*>(sacc + (k * kWave + lane) * VEC);
+        if (n == U) {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int k = 0; k < NCH; ++k)
+#pragma unroll
+              for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+        } else {
+#pragma unroll
+          for (int u = 0; u < U; ++u)
+            if (u < n)
+#pragma unroll
+              for (int k = 0; k < NCH; ++k)
+#pragma unroll
+                for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+        }
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+          *reinterpret_cast<Vec<VEC>*>(sacc + (k * kWave + lane) * VEC) = acc[k];
+        // the next batch's gathers fly while the later waves of this batch add
+        gather(cin, vin);
+        load_idx(b + 2 * B + wave * U, cin, vin);
+      }
+      lds_handover_barrier();
+    }
+  }
+  if (wave != 0) return;
+  float* yrow = Y + static_cast<int64_t>(p) * ldy;
+#pragma unroll
+  for (int k = 0; k < NCH; ++k) {
+    if (!on[k]) continue;
+    Vec<VEC> a = *reinterpret_cast<const Vec<VEC>*>(sacc + (k * kWave + lane) * VEC);
+    if (bias != nullptr) {
+      const Vec<VEC> bv = load_vec<VEC>(bias + col[k]);
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) a.x[q] = a.x[q] + bv.x[q];
+    }
+    if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], a);
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) a.x[q] = apply_act(a.x[q], act);
+    store_vec<VEC>(yrow + col[k], a);
+  }
+}
+
 // Main kernel. One wave per task; grid.y = column panel.
 //   tasks == nullptr : task w = rows of positions [w, w+1)           (plan-less path)
 //   task.w <  0      : rows of positions [task.x, task.y)            (short rows)
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
+// The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
+// (coop_row); the other tasks one wave each, in the blocks after them.
 template <int VEC, int NCH, int U, int WPB = kWavesPerBlock>
 __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
-    const int4* __restrict__ tasks, int n_tasks, const int32_t* __restrict__ indptr,
+    const int4* __restrict__ tasks, int n_tasks, int n_coop, const int32_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
@@ -236,8 +364,6 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int cand = (blk % 8) * per + blk / 8;
     blk = (nb % 8 == 0) ? cand : blk;  // bijective only when 8 divides the grid
   }
-  const int w = uniform(blk * WPB + (threadIdx.x >> 6));
-  if (w >= n_tasks) return;
   const int lane = threadIdx.x & (kWave - 1);
   const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
 
@@ -249,6 +375,14 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     on[k] = col[k] < K;
     gcol[k] = on[k] ? col[k] : panel0;
   }
+  if (blk < n_coop) {  // a whole-workgroup long row (uniform across the block)
+    __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
+    coop_row<VEC, NCH, U, WPB>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z, ldz,
+                               col, gcol, on, Y, ldy, bias, act, gate, ldgate, sacc);
+    return;
+  }
+  const int w = uniform(n_coop + (blk - n_coop) * WPB + (threadIdx.x >> 6));
+  if (w >= n_tasks) return;
 
   int4 t;
   if (tasks != nullptr) {
@@ -359,15 +493,16 @@ struct LaunchArgs {
   int64_t task_nnz;  // plan task size (0 = plan-less, one row per wave)
   uint8_t* gate = nullptr;  // rectify gate bytes (nullable), row stride ldgate
   int64_t ldgate = 0;
+  int n_coop = 0;  // leading tasks run by a whole workgroup each (ordered long rows)
 };
 
 template <int VEC, int NCH, int U, int WPB>
 void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
-  const dim3 grid((a.n_tasks + WPB - 1) / WPB, n_panels);
+  const dim3 grid(a.n_coop + (a.n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
   static const int xcd = env_int("GCG_XCD_REMAP");
   const int nts = env_int("GCG_SPMM_NT_STORE");
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
-                     a.tasks, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
+                     a.tasks, a.n_tasks, a.n_coop, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
                      a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate, a.ldgate, nts);
 }
 
@@ -488,7 +623,20 @@ struct HostPlan {
   std::vector<int32_t> longs;  // quadruples
   int64_t n_slots = 0;
   int64_t max_task_nnz = 0;
+  int64_t n_coop = 0;  // leading tasks that are whole-workgroup rows (ordered mode)
 };
+
+// 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
+// long rows stay single-wave tasks scheduled first. Default 2 x task_nnz; GCG_COOP_MIN = -1
+// disables the cooperative path (experiment knob).
+int64_t coop_min_nnz(int64_t task_nnz) {
+  static const int v = [] {
+    const char* e = std::getenv("GCG_COOP_MIN");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (v < 0) return INT64_MAX;
+  return v > 0 ? v : 2 * task_nnz;
+}
 
 // Default task size: 512 nonzeros, smaller on small graphs so the launch still has
 // >= ~8k waves (256 CUs x 32 waves) to spread; never below 32.
@@ -507,8 +655,11 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   hp->longs.clear();
   hp->n_slots = 0;
   hp->max_task_nnz = 0;
+  hp->n_coop = 0;
+  const int64_t coop_min = coop_min_nnz(task_nnz);
   std::vector<int32_t> seg_tasks;
   std::vector<std::pair<int64_t, int64_t>> long_rows;  // (nnz, position), ordered mode
+  std::vector<std::pair<int64_t, int64_t>> coop_rows;  // (nnz, position), ordered mode
   int64_t cur_begin = -1, cur_cost = 0, cur_nnz = 0;
   auto close = [&](int64_t end) {
     if (cur_begin >= 0) {
@@ -538,9 +689,10 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
     }
     if (ordered && len > task_nnz) {
       // Unsplittable long row (bitwise mode): its own task, scheduled first (LPT) so the
-      // serial tail of a hub row overlaps the bulk instead of ending the launch.
+      // serial tail of a hub row overlaps the bulk instead of ending the launch; the longest
+      // ones on a whole workgroup (coop_row).
       close(p);
-      long_rows.push_back({len, p});
+      (len > coop_min ? coop_rows : long_rows).push_back({len, p});
       continue;
     }
     const int64_t cost = len + kRowCost;
@@ -552,12 +704,17 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   close(n_out);
   // Longest work first: unsplit long rows (ordered mode) by descending length, then the
   // segments of split rows, then the short-row tasks in row order.
-  std::stable_sort(long_rows.begin(), long_rows.end(),
-                   [](const std::pair<int64_t, int64_t>& a, const std::pair<int64_t, int64_t>& b) {
-                     return a.first > b.first;
-                   });
+  auto longest_first = [](const std::pair<int64_t, int64_t>& a,
+                          const std::pair<int64_t, int64_t>& b) { return a.first > b.first; };
+  std::stable_sort(coop_rows.begin(), coop_rows.end(), longest_first);
+  std::stable_sort(long_rows.begin(), long_rows.end(), longest_first);
   std::vector<int32_t> head;
-  head.reserve(long_rows.size() * 4 + seg_tasks.size());
+  head.reserve((coop_rows.size() + long_rows.size()) * 4 + seg_tasks.size());
+  for (const auto& lr : coop_rows) {  // whole-workgroup rows: always the leading tasks
+    head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -2, -1});
+    hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
+  }
+  hp->n_coop = static_cast<int64_t>(coop_rows.size());
   for (const auto& lr : long_rows) {
     head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -1, -1});
     hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
@@ -575,7 +732,7 @@ struct gcg_spmm_plan {
   int64_t n_rows = 0, n_cols = 0, nnz = 0, n_out = 0;
   int ordered = 0;
   int64_t task_nnz = 0;
-  int n_tasks = 0, n_long = 0;
+  int n_tasks = 0, n_long = 0, n_coop = 0;
   int64_t n_slots = 0, max_task_nnz = 0;
   int4* tasks = nullptr;     // device
   int4* longs = nullptr;     // device
@@ -677,6 +834,7 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
   p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz);
   p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
   p->n_long = static_cast<int>(hp.longs.size() / 4);
+  p->n_coop = static_cast<int>(hp.n_coop);
   p->n_slots = hp.n_slots;
   p->max_task_nnz = hp.max_task_nnz;
   auto cleanup = [&]() { gcg_spmm_plan_destroy(p); };
@@ -717,7 +875,7 @@ gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64
                               int64_t* n_segments, int64_t* max_task_nnz) {
   if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
   if (n_tasks) *n_tasks = plan->n_tasks;
-  if (n_long_rows) *n_long_rows = plan->n_long;
+  if (n_long_rows) *n_long_rows = plan->n_long + plan->n_coop;  // split (fast) + whole-workgroup rows (ordered)
   if (n_segments) *n_segments = plan->n_slots;
   if (max_task_nnz) *max_task_nnz = plan->max_task_nnz;
   return GCG_OK;
@@ -753,7 +911,7 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
   float* ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
-               Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate};
+               Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate, plan->n_coop};
   if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
   if (plan->n_long > 0) {
     const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);

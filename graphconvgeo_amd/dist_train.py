@@ -25,6 +25,7 @@ weight gradients differ only by the order of the cross-rank sum.
 """
 from __future__ import annotations
 
+import logging
 import math
 from typing import Optional
 
@@ -38,6 +39,8 @@ from . import sparse as gs
 from .distributed import RowPartitionedCSR
 from .layers import _glorot_uniform, csr_matmul
 from .mlpconv import LasagneAdam
+
+log = logging.getLogger(__name__)
 
 
 class GPUOps:
@@ -124,18 +127,44 @@ def local_targets(idx: np.ndarray, start: int, stop: int):
     return pos, (idx[pos] - start).astype(np.int32)
 
 
+class PartitionTargets:
+    """One target list (train / dev / test indices, the reference's `target_indices`) split
+    over the row partition: rank p keeps the targets in its rows [start, stop), in original
+    order. `rows` are the distinct local rows (increasing) with `weight` their multiplicities
+    (None when no row repeats) and `y` the label of each distinct row; `inverse` maps every kept
+    target to its distinct row, `pos` every kept target to its place in the global list."""
+
+    def __init__(self, idx, y_all, start: int, stop: int, device):
+        idx = np.asarray(idx)
+        self.idx = idx
+        self.total = int(idx.size)
+        self.pos, loc = local_targets(idx, start, stop)
+        uniq, first, inverse, counts = np.unique(loc, return_index=True, return_inverse=True,
+                                                 return_counts=True)
+        self.inverse = torch.as_tensor(inverse.astype(np.int64), device=device)
+        self.rows = gs.RowSelection(uniq.astype(np.int32), device)
+        self.weight = None if uniq.size == loc.size else \
+            torch.as_tensor(counts.astype(np.float32), device=device)
+        self.y = None if y_all is None else torch.as_tensor(
+            np.asarray(y_all)[idx[self.pos][first]].astype(np.int32), device=device)
+
+    def __len__(self):
+        return int(self.pos.size)
+
+
 class RowPartitionedGCN:
     """The MLPCONV network (mlpconv.py:196-217) trained with a 1-D row partition.
 
     Every rank passes the same host H (the normalized operator), X, train indices and labels
     (each rank keeps only its block); parameters are initialised identically (explicit W1/W2
-    or a shared seed) and broadcast from rank 0.
+    or a shared seed) and broadcast from rank 0. Further target lists (dev, test) are added
+    with add_targets(); loss / accuracy / probabilities are per named list.
     """
 
     def __init__(self, H, X, train_indices, y, hidden: int, n_classes: int, rank: int,
                  world: int, device, W1=None, W2=None, order: str = "propagate_first",
                  exchange: str = "auto", mode: str = "auto", regul_coefs=(5e-5, 5e-5),
-                 seed: int = 77, group=None):
+                 seed: int = 77, group=None, rng=None):
         if order not in ("reference", "propagate_first"):
             raise ValueError("order must be 'reference' or 'propagate_first'")
         self.rank, self.world, self.group = rank, world, group
@@ -147,20 +176,13 @@ class RowPartitionedGCN:
         start, stop = self.part.start, self.part.stop
         Xc = sps.csr_matrix(X)[start:stop]
         self.X_p = gs.DeviceCSR.from_scipy(Xc, self.device)
-        idx = np.asarray(train_indices)
-        self.T_total = int(idx.size)
-        pos, loc = local_targets(idx, start, stop)
-        self.rows = gs.RowSelection(loc, self.device)
-        self.y_p = torch.as_tensor(np.asarray(y)[idx[pos]].astype(np.int32), device=self.device)
-        # repeated local targets (drawn with replacement): the output layer runs on the
-        # distinct rows, weighted by multiplicity (MLPCONV._loss_acc does the same)
-        self.row_w = None
-        d = self.rows.distinct()
-        if d is not None:
-            self.rows, first, self.row_w = d
-            self.y_p = self.y_p.index_select(0, first)
+        self.n_classes = int(n_classes)
+        self._y_all = np.asarray(y)
+        self.targets = {}
+        self.add_targets("train", train_indices)
         F = X.shape[1]
-        rng = np.random.RandomState(seed)  # every rank draws the same W1, W2 (then broadcast)
+        # every rank draws the same W1, W2 (then broadcast); rng: a shared RandomState / seed
+        rng = np.random.RandomState(seed) if rng is None else rng
         w1 = torch.as_tensor(_glorot_uniform(F, hidden, rng) if W1 is None else np.asarray(W1))
         w2 = torch.as_tensor(_glorot_uniform(hidden, n_classes, rng) if W2 is None
                              else np.asarray(W2))
@@ -170,33 +192,107 @@ class RowPartitionedGCN:
         self.b2 = torch.nn.Parameter(torch.zeros(n_classes, device=self.device))
         self.params = [self.W1, self.b1, self.W2, self.b2]
         if world > 1:
-            with torch.no_grad():
-                for p in self.params:
-                    dist.broadcast(p.data, src=0, group=group)
+            self.broadcast_params()
         self.proj = dense.Projection()
         sizes = [p.numel() for p in self.params]
         self._bucket = torch.empty(sum(sizes), dtype=torch.float32, device=self.device)
         self._sizes = sizes
 
+    def add_targets(self, name: str, idx, y=None):
+        """Register a target list (the reference's dev / test indices) under `name`; labels from
+        the y given at construction unless `y` (labels of every node) is passed."""
+        self.targets[name] = PartitionTargets(idx, self._y_all if y is None else y,
+                                              self.part.start, self.part.stop, self.device)
+
+    @torch.no_grad()
+    def broadcast_params(self):
+        for p in self.params:
+            dist.broadcast(p.data, src=0, group=self.group)
+
+    # back-compat views of the training list
+    @property
+    def rows(self):
+        return self.targets["train"].rows
+
+    @property
+    def T_total(self):
+        return self.targets["train"].total
+
     # -- forward ------------------------------------------------------------------------
-    def local_loss_acc(self):
-        """This rank's share of (mean CE + penalty, accuracy) over all ranks' targets."""
+    def _hidden(self):
         Z1 = csr_matmul(self.X_p, self.W1, mode=self.mode)  # S.dot(X_p, W1), mlpconv.py:71
-        h = partitioned_propagate(Z1, self.part, self.b1, "relu", None, self.mode)
+        return partitioned_propagate(Z1, self.part, self.b1, "relu", None, self.mode)
+
+    def local_loss_acc(self, name: str = "train", penalty: bool = True):
+        """This rank's share of (mean CE + penalty, accuracy) over all ranks' targets of the
+        list `name` (the mean is over the whole list; the penalty is counted on rank 0)."""
+        tg = self.targets[name]
+        h = self._hidden()
         if self.order == "propagate_first":
-            P = partitioned_propagate(h, self.part, None, None, self.rows, self.mode)
-            loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, self.y_p, denom=self.T_total,
-                                               row_weight=self.row_w)
+            P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+            loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, tg.y, denom=tg.total,
+                                               row_weight=tg.weight)
         else:
             Z2 = dense.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
-            logits = partitioned_propagate(Z2, self.part, self.b2, None, self.rows, self.mode)
-            loss, acc = dense.softmax_xent(logits, self.y_p, denom=self.T_total,
-                                           row_weight=self.row_w)
-        if self.rank == 0:
+            logits = partitioned_propagate(Z2, self.part, self.b2, None, tg.rows, self.mode)
+            loss, acc = dense.softmax_xent(logits, tg.y, denom=tg.total, row_weight=tg.weight)
+        if penalty and self.rank == 0:
             c_out, c_hid = self.regul_coefs  # mlpconv.py:235-243, counted once
             loss = loss + dense.l1l2_penalty([self.W2, self.W1], [(c_out * 0.5, c_out * 0.5),
                                                                    (c_hid * 0.5, c_hid * 0.5)])
         return loss, acc
+
+    def _allreduce(self, t: torch.Tensor) -> torch.Tensor:
+        if self.world > 1:
+            dist.all_reduce(t, group=self.group)
+        return t
+
+    @torch.no_grad()
+    def evaluate(self, name: str, penalty: bool = True):
+        """Global (loss, acc) of the list `name` (forward only, all-reduced), as device scalars."""
+        loss, acc = self.local_loss_acc(name, penalty=penalty)
+        stats = self._allreduce(torch.stack([loss.detach().reshape(()), acc.detach().reshape(())]))
+        return stats[0], stats[1]
+
+    @torch.no_grad()
+    def local_probabilities(self, name: str) -> torch.Tensor:
+        """softmax rows of this rank's kept targets of `name`, in their global order."""
+        tg = self.targets[name]
+        h = self._hidden()
+        if self.order == "propagate_first" and self.n_classes <= dense.FUSED_MAX_COLS:
+            P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+            probs = self.proj.probabilities(P, self.W2, self.b2)
+        else:
+            if self.order == "propagate_first":
+                P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+                logits = dense.matmul(P, self.W2, self.b2)
+            else:
+                Z2 = dense.matmul(h, self.W2)
+                logits = partitioned_propagate(Z2, self.part, self.b2, None, tg.rows, self.mode)
+            probs = dense.softmax(logits)
+        return probs.index_select(0, tg.inverse)
+
+    @torch.no_grad()
+    def gather_probabilities(self, name: str, dst: int = 0):
+        """The whole list's probabilities [T, C] (original target order) on rank `dst` only
+        (None elsewhere): each rank sends its kept rows, padded to the largest share."""
+        tg = self.targets[name]
+        local = self.local_probabilities(name).contiguous()
+        if self.world == 1:
+            return local.cpu().numpy()
+        b = self.part.bounds
+        shares = [local_targets(tg.idx, int(b[q]), int(b[q + 1]))[0] for q in range(self.world)]
+        m = max(max(x.size for x in shares), 1)
+        send = torch.zeros((m, self.n_classes), dtype=torch.float32, device=self.device)
+        send[: len(tg)] = local
+        recv = [torch.empty_like(send) for _ in range(self.world)] if self.rank == dst else None
+        dist.gather(send, recv, dst=dst, group=self.group)
+        if self.rank != dst:
+            return None
+        out = np.empty((tg.total, self.n_classes), dtype=np.float32)
+        for q, pos in enumerate(shares):
+            out[pos] = recv[q][: pos.size].cpu().numpy()
+        return out
 
     # -- one optimisation step -----------------------------------------------------------
     def allreduce_grads(self):
@@ -205,8 +301,7 @@ class RowPartitionedGCN:
         for p, n in zip(self.params, self._sizes):
             self._bucket[off:off + n].copy_(p.grad.reshape(-1))
             off += n
-        if self.world > 1:
-            dist.all_reduce(self._bucket, group=self.group)
+        self._allreduce(self._bucket)
         off = 0
         for p, n in zip(self.params, self._sizes):
             p.grad.copy_(self._bucket[off:off + n].view_as(p.grad))
@@ -222,13 +317,162 @@ class RowPartitionedGCN:
                 p.grad = torch.zeros_like(p)
         self.allreduce_grads()
         opt.step()
-        stats = torch.stack([loss.detach(), acc.detach()])
-        if self.world > 1:
-            dist.all_reduce(stats, group=self.group)
+        stats = self._allreduce(torch.stack([loss.detach(), acc.detach()]))
         return stats[0], stats[1]
 
     def make_optimizer(self, lr=4e-3) -> LasagneAdam:
         return LasagneAdam(self.params, lr=lr, beta1=0.9, beta2=0.999, epsilon=1e-8)
+
+
+class RowPartitionedMLPCONV:
+    """MLPCONV.fit / predict / predict_proba / accuracy / score (mlpconv.py:152-349) over a
+    1-D row partition: one process per GPU, every rank calls the same methods with the same
+    host arguments (each keeps its block). Same constructor arguments as MLPCONV plus
+    rank / world / group / exchange; the epoch loop, validation every report_k_epoch,
+    best-parameter restore, early stopping and the final dev evaluation follow MLPCONV.fit
+    (graphconvgeo_amd/mlpconv.py), with every loss and hit count all-reduced so that every rank
+    takes the same decisions. predict / predict_proba return the requested partition's rows on
+    rank 0 (None on the other ranks); accuracy and score are global on every rank."""
+
+    def __init__(self, n_epochs=10, batch_size=1000, init_parameters=None, complete_prob=False,
+                 add_hidden=True, regul_coefs=(5e-5, 5e-5), save_results=False,
+                 hidden_layer_size=None, drop_out=False, dropout_coefs=(0.5, 0.5),
+                 early_stopping_max_down=100000, loss_name="log", nonlinearity="rectify",
+                 dtype="float32", device="cuda", seed: Optional[int] = None, mode: str = "auto",
+                 model_file: Optional[str] = None, report_k_epoch: int = 10,
+                 order: str = "reference", rank: Optional[int] = None,
+                 world: Optional[int] = None, group=None, exchange: str = "auto",
+                 network_factory=None):
+        if dtype != "float32":
+            raise ValueError("the GPU path computes in float32 (mlpconv.py dtype='float32')")
+        if drop_out:
+            raise NotImplementedError("dropout is out of scope (main_mlpconv uses drop_out=False)")
+        if complete_prob:
+            raise NotImplementedError("complete_prob (soft labels) is not on the graded path")
+        if loss_name != "log":
+            raise ValueError("only the 'log' (categorical cross-entropy) loss exists in the reference")
+        if order not in ("reference", "propagate_first", "auto"):
+            raise ValueError("order must be 'reference', 'propagate_first' or 'auto'")
+        self.n_epochs = n_epochs
+        self.batch_size = batch_size
+        self.init_parameters = init_parameters
+        self.regul_coefs = list(regul_coefs)
+        self.hidden_layer_size = hidden_layer_size
+        self.dropout_coefs = list(dropout_coefs)
+        self.early_stopping_max_down = early_stopping_max_down
+        self.device = torch.device(device)
+        self.seed, self.mode, self.order = seed, mode, order
+        self.model_file = model_file
+        self.report_k_epoch = report_k_epoch
+        self.rank = dist.get_rank(group) if rank is None else rank
+        self.world = dist.get_world_size(group) if world is None else world
+        self.group, self.exchange = group, exchange
+        self.network_factory = network_factory or RowPartitionedGCN
+        self.history = []
+
+    def fit(self, X, train_indices, dev_indices, test_indices, Y, H):
+        """mlpconv.py:152-318 over the row partition (full-batch epochs)."""
+        Y = np.asarray(Y)
+        if Y.ndim != 1 or not np.issubdtype(Y.dtype, np.integer):
+            raise ValueError("Y must be a 1-D integer label array (complete_prob is out of scope)")
+        if Y.size and int(Y.min()) < 0:
+            raise ValueError("labels must be >= 0 (class ids, data.py:399-432)")
+        if self.hidden_layer_size is None:
+            raise ValueError("hidden_layer_size is required")
+        out_size = int(np.max(Y)) + 1
+        order = self.order
+        if order == "auto":  # as ConvolutionDenseLayer(order="auto")
+            order = "propagate_first" if out_size > self.hidden_layer_size else "reference"
+        W1 = W2 = None
+        if self.init_parameters is not None:
+            W1, _b1, W2, _b2 = self.init_parameters
+        # Lasagne GlorotUniform from numpy's global stream (W1 then W2) unless a seed is given;
+        # every rank draws, rank 0's draw is broadcast
+        rng = np.random.mtrand._rand if self.seed is None else np.random.RandomState(self.seed)
+        idx = {"train": np.asarray(train_indices, np.int32), "dev": np.asarray(dev_indices, np.int32),
+               "test": np.asarray(test_indices, np.int32)}
+        net = self.network_factory(H, X, idx["train"], Y, hidden=self.hidden_layer_size,
+                                   n_classes=out_size, rank=self.rank, world=self.world,
+                                   device=self.device, W1=W1, W2=W2, order=order,
+                                   exchange=self.exchange, mode=self.mode,
+                                   regul_coefs=self.regul_coefs, group=self.group, rng=rng)
+        for k in ("dev", "test"):
+            net.add_targets(k, idx[k])
+        if self.init_parameters is not None:
+            with torch.no_grad():
+                net.b1.copy_(torch.as_tensor(self.init_parameters[1]))
+                net.b2.copy_(torch.as_tensor(self.init_parameters[3]))
+        self.net = net
+        self.params = net.params
+        opt = net.make_optimizer()
+        self.optimizer = opt
+        best_params, best_val_loss, best_val_acc, n_down = None, math.inf, 0.0, 0
+        for n in range(self.n_epochs):
+            loss, acc = net.train_step(opt)
+            rec = {"epoch": n, "train_loss": float(loss), "train_acc": float(acc)}
+            if n % self.report_k_epoch == 0:
+                l_val, a_val = (float(x) for x in net.evaluate("dev"))
+                rec.update(val_loss=l_val, val_acc=a_val)
+                if l_val < best_val_loss:
+                    best_val_loss, best_val_acc, n_down = l_val, a_val, 0
+                    best_params = [p.detach().clone() for p in self.params]
+                else:
+                    n_down += 1
+                log.info("epoch %d ,train_loss %s ,acc %s ,val_loss %s ,acc %s,best_val_acc %s",
+                         n, rec["train_loss"], rec["train_acc"], l_val, a_val, best_val_acc)
+                self.history.append(rec)
+                if n_down > self.early_stopping_max_down:
+                    log.info("validation results went down. early stopping ...")
+                    break
+            else:
+                self.history.append(rec)
+        if best_params is not None:
+            with torch.no_grad():
+                for p, b in zip(self.params, best_params):
+                    p.copy_(b)
+        if self.model_file and self.rank == 0:
+            torch.save([p.detach().cpu() for p in self.params], self.model_file)
+            self.model_path = self.model_file
+        l_val, a_val = net.evaluate("dev")  # final dev evaluation, mlpconv.py:316-318
+        self.best_dev_loss, self.best_dev_acc = float(l_val), float(a_val)
+        log.info("Best dev acc: %f", self.best_dev_acc)
+        return self
+
+    def _check(self, partition):
+        if partition not in ("train", "dev", "test"):
+            raise ValueError(f"unknown partition {partition!r}")
+
+    def predict_proba(self, dataset_partition):
+        self._check(dataset_partition)
+        return self.net.gather_probabilities(dataset_partition, dst=0)
+
+    def predict(self, dataset_partition):
+        proba = self.predict_proba(dataset_partition)
+        return None if proba is None else proba.argmax(axis=1)
+
+    def accuracy(self, dataset_partition, y_true):
+        """Global accuracy of the partition against y_true (the labels of its targets, in
+        target order), on every rank."""
+        self._check(dataset_partition)
+        idx = self.net.targets[dataset_partition].idx
+        y_true = np.asarray(y_true)
+        if y_true.shape != idx.shape:
+            raise ValueError("y_true must hold one label per target of the partition")
+        y_all = np.zeros(self.net.part.n, dtype=np.int64)
+        y_all[idx] = y_true
+        self.net.add_targets("_accuracy", idx, y_all)
+        try:
+            _loss, acc = self.net.evaluate("_accuracy", penalty=False)
+        finally:
+            del self.net.targets["_accuracy"]
+        return float(acc)
+
+    def score(self, X, dataset_partition, y_true):
+        """mlpconv.py:348-349 signature (see MLPCONV.score)."""
+        return self.accuracy(dataset_partition, y_true)
+
+    def get_params(self):
+        return [p.detach().cpu().numpy() for p in self.params]
 
 
 def spmm_bytes_per_step(part: RowPartitionedCSR, X_p: gs.DeviceCSR, K: int, n_targets: int,

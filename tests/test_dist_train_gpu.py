@@ -95,3 +95,67 @@ def test_row_partitioned_training_matches_oracle(cuda, order, exchange):
     # trajectory above is the parity check; here only a loose bound (8 steps x lr = 0.032)
     for p, k in zip(params, ("W1", "b1", "W2", "b2")):
         assert np.abs(p - ref_params[k]).max() < 0.02, k
+
+
+def _fit_worker(rank, world, port, order, q):
+    import torch
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphconvgeo_amd.dist_train import RowPartitionedMLPCONV
+        H, X, Y, train, dev, test, init = problem(c=60)
+        clf = RowPartitionedMLPCONV(n_epochs=21, hidden_layer_size=48, regul_coefs=(1e-5, 1e-5),
+                                    init_parameters=init, device="cuda:0", report_k_epoch=5,
+                                    order=order, early_stopping_max_down=100)
+        clf.fit(X, train, dev, test, Y, H)
+        proba = clf.predict_proba("test")
+        pred = clf.predict("test")
+        acc = clf.accuracy("test", Y[test])
+        torch.cuda.synchronize()
+        q.put((rank, clf.history, clf.best_dev_loss, clf.best_dev_acc, proba, pred, acc,
+               clf.get_params()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("order", ["propagate_first", "reference"])
+def test_row_partitioned_fit_matches_mlpconv(cuda, order):
+    """RowPartitionedMLPCONV.fit (2 ranks over gloo sharing one MI355X, every product in the
+    HIP kernels) against single-process MLPCONV.fit on the same data and initial parameters
+    (mlpconv.py:152-349): loss / accuracy history within 1e-4, the same best dev accuracy,
+    identical test predictions gathered on rank 0, the same global accuracy on both ranks."""
+    from graphconvgeo_amd.mlpconv import MLPCONV
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fit_worker, args=(r, world, port, order, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=240) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, hist, bl, ba, proba, pred, acc, params), (_, hist1, bl1, ba1, proba1, pred1, acc1, params1) = out
+    assert hist == hist1 and bl == bl1 and ba == ba1 and acc == acc1 and proba1 is None
+    assert all(np.array_equal(a, b) for a, b in zip(params, params1))  # replicas identical
+    H, X, Y, train, dev, test, init = problem(c=60)
+    ref = MLPCONV(n_epochs=21, hidden_layer_size=48, regul_coefs=(1e-5, 1e-5), init_parameters=init,
+                  device=cuda, report_k_epoch=5, order=order, early_stopping_max_down=100)
+    ref.fit(X, train, dev, test, Y, H)
+    assert [h["epoch"] for h in hist] == [h["epoch"] for h in ref.history]
+    for key in ("train_loss", "val_loss"):
+        got = np.array([h[key] for h in hist if key in h])
+        want = np.array([h[key] for h in ref.history if key in h])
+        assert np.abs(got - want).max() < 1e-4 * max(1.0, np.abs(want).max()), (key, got, want)
+    for key in ("train_acc", "val_acc"):
+        got = np.array([h[key] for h in hist if key in h])
+        want = np.array([h[key] for h in ref.history if key in h])
+        assert np.abs(got - want).max() <= 2.0 / len(dev), key  # argmax ties at f32 rounding
+    assert abs(ba - ref.best_dev_acc) <= 2.0 / len(dev)
+    want_proba = ref.predict_proba("test")
+    assert proba.shape == want_proba.shape
+    assert np.abs(proba - want_proba).max() < 1e-4
+    assert np.array_equal(pred, ref.predict("test"))
+    assert abs(acc - ref.accuracy("test", Y[test])) <= 1e-6

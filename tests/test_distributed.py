@@ -223,3 +223,126 @@ def test_local_targets_keeps_order_and_duplicates():
     from graphconvgeo_amd.dist_train import local_targets
     pos, loc = local_targets(np.array([5, 1, 7, 5, 3, 9]), 3, 8)
     assert pos.tolist() == [0, 2, 3, 4] and loc.tolist() == [2, 4, 2, 0]
+
+
+def _fit_loop_worker(rank, world, port, q):
+    """RowPartitionedMLPCONV.fit's loop and the partition's probability gather over gloo, with a
+    scripted CPU network in place of the HIP one (the numerics are tests/test_dist_train_gpu.py)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import scipy.sparse as sps
+        from graphconvgeo_amd.dist_train import RowPartitionedGCN, RowPartitionedMLPCONV
+        from graphconvgeo_amd.distributed import row_partition
+
+        VAL = [5.0, 4.0, 3.0, 3.5, 3.2, 3.9, 4.0, 4.1, 4.2]  # dev loss at epochs 0, 5, 10, ...
+
+        class _Part:
+            def __init__(self, H, rank, world):
+                self.n = H.shape[0]
+                self.bounds = row_partition(H.indptr, world)
+                self.start, self.stop = int(self.bounds[rank]), int(self.bounds[rank + 1])
+
+        class ScriptedNet(RowPartitionedGCN):
+            def __init__(self, H, X, train_idx, Y, hidden, n_classes, rank, world, device,
+                         group=None, **kw):
+                self.rank, self.world, self.group = rank, world, group
+                self.device = torch.device(device)
+                self.part = _Part(H, rank, world)
+                self.n_classes = n_classes
+                self._y_all = np.asarray(Y)
+                self.targets = {}
+                self.add_targets("train", train_idx)
+                self.W = torch.nn.Parameter(torch.zeros(2))
+                self.b1 = torch.nn.Parameter(torch.zeros(1))
+                self.b2 = torch.nn.Parameter(torch.zeros(1))
+                self.params = [self.W, self.b1, self.W, self.b2]
+                self.epoch = 0
+
+            def make_optimizer(self, lr=4e-3):
+                return None
+
+            def train_step(self, opt):
+                with torch.no_grad():
+                    self.W += 1.0  # the parameters after epoch n hold n + 1
+                self.epoch += 1
+                # each rank's share: its targets / total -> the all-reduced mean is 1.0
+                share = torch.tensor([len(self.targets["train"]) / self.targets["train"].total,
+                                      0.5 * len(self.targets["train"]) / self.targets["train"].total])
+                dist.all_reduce(share)
+                return share[0], share[1]
+
+            def evaluate(self, name, penalty=True):
+                k = (self.epoch - 1) // 5
+                v = torch.tensor([VAL[min(k, len(VAL) - 1)] / self.world, 0.1 * k / self.world])
+                dist.all_reduce(v)
+                if name == "_accuracy":  # accuracy(): fraction of hits of the given labels
+                    tg = self.targets[name]
+                    hits = (tg.y.to(torch.float64) == 1).to(torch.float64)
+                    w = tg.weight.to(torch.float64) if tg.weight is not None else 1.0
+                    a = torch.tensor([float((hits * w).sum()) / tg.total], dtype=torch.float64)
+                    dist.all_reduce(a)
+                    return v[0], a[0]
+                return v[0], v[1]
+
+            def local_probabilities(self, name):
+                tg = self.targets[name]
+                node = torch.as_tensor(tg.idx[tg.pos], dtype=torch.float32)
+                out = torch.zeros((len(tg), self.n_classes))
+                out[:, 0] = node
+                out[:, 1] = float(self.rank)
+                out[torch.arange(len(tg)), 2 + (tg.idx[tg.pos] % (self.n_classes - 2))] = 1e3
+                return out
+
+        H = synthetic_graph(600, 3000)
+        X = sps.random(600, 20, density=0.1, format="csr", random_state=1, dtype=np.float32)
+        Y = np.random.default_rng(2).integers(0, 6, size=600)
+        train = np.random.default_rng(3).choice(400, 500).astype(np.int32)  # with replacement
+        dev_i = np.arange(400, 500, dtype=np.int32)
+        test_i = np.random.default_rng(4).permutation(600)[:70].astype(np.int32)
+        clf = RowPartitionedMLPCONV(n_epochs=40, hidden_layer_size=4, report_k_epoch=5,
+                                    early_stopping_max_down=3, device="cpu",
+                                    network_factory=ScriptedNet)
+        clf.fit(X, train, dev_i, test_i, Y, H)
+        proba = clf.predict_proba("test")
+        pred = clf.predict("test")
+        acc = clf.accuracy("test", (Y[test_i] == 1).astype(np.int64))
+        q.put((rank, clf.history, float(clf.params[0].detach()[0]), clf.best_dev_loss, proba, pred, acc))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_row_partitioned_fit_loop_and_gather():
+    """RowPartitionedMLPCONV.fit over gloo world-2: validation every report_k_epoch from the
+    all-reduced dev loss, best-parameter restore, early stopping after early_stopping_max_down
+    non-improving validations (mlpconv.py:296-318 as graphconvgeo_amd.mlpconv.MLPCONV.fit does
+    it), identical on both ranks; predict_proba gathers the test rows to rank 0 in the original
+    target order; accuracy is the global hit fraction on every rank."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fit_loop_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    out = sorted((q.get(timeout=120) for _ in range(world)), key=lambda r: r[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    (_, hist0, w0, best0, proba0, pred0, acc0), (_, hist1, w1, best1, proba1, pred1, acc1) = out
+    assert hist0 == hist1 and w0 == w1 and best0 == best1 and acc0 == acc1
+    vals = [h["val_loss"] for h in hist0 if "val_loss" in h]
+    # dev losses 5, 4, 3 (best, epoch 10), then 3.5, 3.2, 3.9 -> 3 non-improving, then 4.0 is
+    # the 4th: n_down 4 > 3 stops at epoch 30
+    assert [round(v, 6) for v in vals] == [5.0, 4.0, 3.0, 3.5, 3.2, 3.9, 4.0]
+    assert hist0[-1]["epoch"] == 30 and len(hist0) == 31
+    assert all(abs(h["train_loss"] - 1.0) < 1e-6 and abs(h["train_acc"] - 0.5) < 1e-6
+               for h in hist0)
+    assert w0 == 11.0  # parameters restored to the ones after epoch 10
+    assert proba1 is None and pred1 is None
+    test_i = np.random.default_rng(4).permutation(600)[:70]
+    assert np.array_equal(proba0[:, 0], test_i.astype(np.float32))  # original target order
+    assert set(np.unique(proba0[:, 1])) == {0.0, 1.0}  # rows from both ranks
+    assert np.array_equal(pred0, 2 + test_i % 4)
+    Y = np.random.default_rng(2).integers(0, 6, size=600)
+    assert abs(acc0 - float((Y[test_i] == 1).mean())) < 1e-6

@@ -297,3 +297,44 @@ def test_rows_transpose_equals_scipy(cuda):
     assert np.abs(got - O.spmm_f32(H, full)).max() < 1e-5
     empty = A.rows_transpose(gs.RowSelection(np.zeros(0, np.int32), cuda))
     assert empty.shape == (5000, 0) and empty.nnz == 0
+
+
+@pytest.mark.parametrize("K", [1, 3, 64, 65, 300, 513, 930])
+@pytest.mark.parametrize("task_nnz", [32, 128, 512])
+def test_ordered_cooperative_long_rows_bitwise(cuda, K, task_nnz):
+    """'ordered' rows longer than 2 x task_nnz run on a whole workgroup (spmm.hip coop_row:
+    the storage-order sum handed from wave to wave through LDS). Rows of every length around
+    the batch size (WPB x U), a row subset repeating the long rows, bias + rectify + gate:
+    bitwise the oracle."""
+    lens = [(3, 5000), (10, 2 * task_nnz + 1), (11, 64 * 3 + 17), (12, 64), (13, 65), (14, 4097),
+            (20, 12189)]
+    H = rand_csr(400, 30000, 10, seed=K + task_nnz, long_rows=lens)  # wide: few duplicates
+    Z = np.random.default_rng(K).standard_normal((30000, K)).astype(np.float32)
+    b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    info = A.plan(None, True, task_nnz).info()
+    assert info["n_long_rows"] == int((np.diff(H.indptr) > 2 * task_nnz).sum()) >= 3
+    Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered", task_nnz=task_nnz).cpu().numpy()
+    assert np.array_equal(Y, O.spmm_f32(H, Z))
+    rows = np.array([20, 3, 3, 7, 14, 10, 20, 0, 11, 12, 13], np.int32)
+    gate = gs.empty_gate(rows.size, K, cuda)
+    Yr = gs.spmm(A, to_dev(Z, cuda), bias=to_dev(b, cuda), act="relu", rows=gs.RowSelection(rows, cuda),
+                 mode="ordered", task_nnz=task_nnz, gate=gate).cpu().numpy()
+    pre = O.spmm_f32(H, Z, bias=b, rows=rows)
+    assert np.array_equal(Yr, O.relu(pre))
+    assert np.array_equal(gate.cpu().numpy(), (2 * (pre > 0) + (pre == 0)).astype(np.uint8))
+
+
+def test_ordered_cooperative_world_scale_block(cuda):
+    """A Twitter-World-like power-law block (hub rows of ~12k nonzeros) in 'ordered' mode:
+    every hub row on the cooperative path, sampled rows bitwise the oracle, hub rows included."""
+    H = synthetic_graph(200_000, 3_000_000)
+    n = H.shape[0]
+    Z = dense(n, 300)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    assert A.plan(None, True, 0).info()["n_long_rows"] > 0
+    Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered").cpu().numpy()
+    lens = np.diff(H.indptr)
+    hubs = np.argsort(lens)[-64:]
+    sample = np.unique(np.concatenate([hubs, np.random.default_rng(0).choice(n, 2000)]))
+    assert np.array_equal(Y[sample], O.spmm_f32(H, Z, rows=sample))
