@@ -283,6 +283,33 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
       for (int k = 0; k < NCH; ++k) z[u][k] = load_vec<VEC>(zrow + gcol[k]);
     }
   };
+  // products v * z formed in place (z <- v * z, rounded as in acc + v * z), then added in
+  // storage order; both as packed f32 ops where VEC allows (v_pk_mul_f32 / v_pk_add_f32: half
+  // the VALU issue of a hand-over stage, which the waves of a batch take in turn)
+  auto multiply = [&]() {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+      for (int k = 0; k < NCH; ++k)
+#pragma unroll
+        for (int q = 0; q < VEC; ++q) z[u][k].x[q] = v[u] * z[u][k].x[q];
+  };
+  auto add = [&](Vec<VEC>& a, const Vec<VEC>& t) {
+    if constexpr (VEC % 2 == 0) {  // packed f32 adds (v_pk_add_f32), each lane rounded alone
+      typedef float f2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int q = 0; q < VEC; q += 2) {
+        f2v x = {a.x[q], a.x[q + 1]};
+        const f2v y = {t.x[q], t.x[q + 1]};
+        x = x + y;
+        a.x[q] = x[0];
+        a.x[q + 1] = x[1];
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) a.x[q] = a.x[q] + t.x[q];
+    }
+  };
   int ci, cin;
   float vi, vin;
   load_idx(s + wave * U, ci, vi);
@@ -297,21 +324,18 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
           acc[k] = *reinterpret_cast<const Vec<VEC>*>(sacc + (k * kWave + lane) * VEC);
+        multiply();
         if (n == U) {
 #pragma unroll
           for (int u = 0; u < U; ++u)
 #pragma unroll
-            for (int k = 0; k < NCH; ++k)
-#pragma unroll
-              for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+            for (int k = 0; k < NCH; ++k) add(acc[k], z[u][k]);
         } else {
 #pragma unroll
           for (int u = 0; u < U; ++u)
             if (u < n)
 #pragma unroll
-              for (int k = 0; k < NCH; ++k)
-#pragma unroll
-                for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + v[u] * z[u][k].x[q];
+              for (int k = 0; k < NCH; ++k) add(acc[k], z[u][k]);
         }
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
@@ -627,15 +651,20 @@ struct HostPlan {
 };
 
 // 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
-// long rows stay single-wave tasks scheduled first. Default 2 x task_nnz; GCG_COOP_MIN = -1
-// disables the cooperative path (experiment knob).
+// long rows stay single-wave tasks scheduled first. Default 8 x task_nnz (4096 at Twitter-World);
+// GCG_COOP_MIN = -1 disables the cooperative path (experiment knob). Measured (World power-law,
+// K = 300, slowest of P row blocks, tools/exp_block_modes.py): P = 4 2.12 -> 1.70 ms, P = 8
+// 1.59 -> 1.16 ms, P = 1 and 2 unchanged; thresholds 1024 / 2048 / 4096 within noise of each
+// other. One hub row alone is bound by its CU (~19 GB/s per CU for 1216-B random rows: 0.77 ms
+// for 12,189 nonzeros on 4 waves vs 0.83 on one), so the gain is that hub rows now get a CU
+// each instead of sharing one four to a workgroup.
 int64_t coop_min_nnz(int64_t task_nnz) {
   static const int v = [] {
     const char* e = std::getenv("GCG_COOP_MIN");
     return e ? std::atoi(e) : 0;
   }();
   if (v < 0) return INT64_MAX;
-  return v > 0 ? v : 2 * task_nnz;
+  return v > 0 ? v : 8 * task_nnz;
 }
 
 // Default task size: 512 nonzeros, smaller on small graphs so the launch still has

@@ -302,21 +302,21 @@ def test_rows_transpose_equals_scipy(cuda):
 @pytest.mark.parametrize("K", [1, 3, 64, 65, 300, 513, 930])
 @pytest.mark.parametrize("task_nnz", [32, 128, 512])
 def test_ordered_cooperative_long_rows_bitwise(cuda, K, task_nnz):
-    """'ordered' rows longer than 2 x task_nnz run on a whole workgroup (spmm.hip coop_row:
+    """'ordered' rows longer than 8 x task_nnz run on a whole workgroup (spmm.hip coop_row:
     the storage-order sum handed from wave to wave through LDS). Rows of every length around
     the batch size (WPB x U), a row subset repeating the long rows, bias + rectify + gate:
     bitwise the oracle."""
-    lens = [(3, 5000), (10, 2 * task_nnz + 1), (11, 64 * 3 + 17), (12, 64), (13, 65), (14, 4097),
-            (20, 12189)]
+    lens = [(3, 5000), (10, 8 * task_nnz + 1), (11, 8 * task_nnz + 64 * 3 + 17), (12, 8 * task_nnz + 64),
+            (13, 8 * task_nnz + 65), (14, 4097), (20, 12189), (21, 8 * task_nnz)]
     H = rand_csr(400, 30000, 10, seed=K + task_nnz, long_rows=lens)  # wide: few duplicates
     Z = np.random.default_rng(K).standard_normal((30000, K)).astype(np.float32)
     b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
     A = gs.DeviceCSR.from_scipy(H, cuda)
     info = A.plan(None, True, task_nnz).info()
-    assert info["n_long_rows"] == int((np.diff(H.indptr) > 2 * task_nnz).sum()) >= 3
+    assert info["n_long_rows"] == int((np.diff(H.indptr) > 8 * task_nnz).sum()) >= 3
     Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered", task_nnz=task_nnz).cpu().numpy()
     assert np.array_equal(Y, O.spmm_f32(H, Z))
-    rows = np.array([20, 3, 3, 7, 14, 10, 20, 0, 11, 12, 13], np.int32)
+    rows = np.array([20, 3, 3, 7, 14, 10, 20, 0, 11, 12, 13, 21], np.int32)
     gate = gs.empty_gate(rows.size, K, cuda)
     Yr = gs.spmm(A, to_dev(Z, cuda), bias=to_dev(b, cuda), act="relu", rows=gs.RowSelection(rows, cuda),
                  mode="ordered", task_nnz=task_nnz, gate=gate).cpu().numpy()
