@@ -308,12 +308,12 @@ def test_ordered_cooperative_long_rows_bitwise(cuda, K, task_nnz):
     bitwise the oracle."""
     lens = [(3, 5000), (10, 8 * task_nnz + 1), (11, 8 * task_nnz + 64 * 3 + 17), (12, 8 * task_nnz + 64),
             (13, 8 * task_nnz + 65), (14, 4097), (20, 12189), (21, 8 * task_nnz)]
-    H = rand_csr(400, 30000, 10, seed=K + task_nnz, long_rows=lens)  # wide: few duplicates
+    H = rand_csr(400, 30000, 10, seed=K + task_nnz, long_rows=lens, dups=True)  # exact lengths
     Z = np.random.default_rng(K).standard_normal((30000, K)).astype(np.float32)
     b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
     A = gs.DeviceCSR.from_scipy(H, cuda)
     info = A.plan(None, True, task_nnz).info()
-    assert info["n_long_rows"] == int((np.diff(H.indptr) > 8 * task_nnz).sum()) >= 3
+    assert info["n_long_rows"] == int((np.diff(H.indptr) > 8 * task_nnz).sum()) >= 4
     Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered", task_nnz=task_nnz).cpu().numpy()
     assert np.array_equal(Y, O.spmm_f32(H, Z))
     rows = np.array([20, 3, 3, 7, 14, 10, 20, 0, 11, 12, 13, 21], np.int32)
