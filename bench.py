@@ -246,6 +246,21 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     return out
 
 
+def spmm_mode_variant(A, H, K: int, mode: str, reps: int, dev) -> dict:
+    """The headline SpMM (same graph, K) in another mode."""
+    g = torch.Generator(device=dev).manual_seed(SEED)
+    Z = gs.empty_dense(H.shape[0], K, dev).copy_(torch.randn((H.shape[0], K), generator=g, device=dev))
+    Y = gs.empty_dense(H.shape[0], K, dev)
+    gs.spmm(A, Z, out=Y, mode=mode)
+    k_ms = time_events(lambda: gs.spmm(A, Z, out=Y, mode=mode), reps, dev)
+    B = spmm_bytes(H.shape[0], H.nnz, K)
+    gbs = B / (k_ms * 1e-3) / 1e9
+    del Z, Y
+    return {"graph": "powerlaw (the headline graph)", "mode": mode, "kernel_ms": round(k_ms, 3),
+            "value": round(gbs, 1), "unit": "GB/s", "edges_per_s": round(H.nnz / (k_ms * 1e-3), 1),
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "algorithmic_bytes_per_launch": B}
+
+
 def spmm_wide_variant(A, N: int, nnz: int, K: int, mode: str, reps: int, dev) -> dict:
     """the same World SpMM at the wider hidden size K = 1500
     (tensormain.py:398), on the headline graph already resident in HBM."""
@@ -435,7 +450,8 @@ def main():
         part = RowPartitionedCSR(H, rank, world, dev, exchange=args.exchange)
         Zl = torch.randn((part.local_block_rows, K), generator=gen, device=dev, dtype=torch.float32)
         Y = gs.empty_dense(part.n_local, K, dev)
-        eff = resolve_mode(part.A, args.mode)
+        # one mode for every rank, resolved from all row blocks (RowPartitionedCSR.resolve_mode)
+        eff = part.resolve_mode(args.mode)
         part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
         info = part.A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
 
@@ -567,6 +583,9 @@ def main():
         "edges_per_s": round(nnz / (ms * 1e-3)),
         "config": {"workload": f"{cfg.name} H.Z SpMM fwd, {args.graph} degrees", "nodes": N,
                    "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": f"{args.mode}->{eff}",
+                   "mode_resolution": ("global over the row blocks: " + ",".join(
+                       getattr(part, "block_modes", [])) if (world > 1 or args.partitioned)
+                                       else "the whole graph (sparse.resolve_auto)"),
                    "parallelism": f"row{world}" if world > 1 else "single",
                    "plan": info, "graph_gen_s": round(t_gen, 1)},
     }
@@ -584,6 +603,11 @@ def main():
         if args.graph == "powerlaw" and K != 1500:
             rec["variants"]["k1500"] = spmm_wide_variant(A, N, nnz, 1500, eff,
                                                          max(args.steps // 4, 3), dev)
+        if eff != "fast":
+            # the same SpMM in 'fast' mode (hub rows split, within 1e-5): the arithmetic the
+            # N > 1 lines run when a row block's hub rows force it (RowPartitionedCSR.resolve_mode),
+            # so the scaling series has a like-for-like N = 1 point
+            rec["variants"]["fast"] = spmm_mode_variant(A, H, K, "fast", max(args.steps, 5), dev)
     if world == 1 and not args.partitioned and args.dense:
         rec["dense_kernels"] = dense_kernels_bench(max(args.steps // 2, 5), dev)
     if world == 1 and not args.partitioned and args.train_step:

@@ -64,6 +64,7 @@ class RowPartitionedCSR:
             raise ValueError("exchange must be 'auto', 'allgather' or 'halo'")
         self.rank, self.world, self.group = rank, world, group
         self.n = H.shape[0]
+        self._indptr_host = H.indptr
         self.bounds = row_partition(H.indptr, world) if bounds is None else np.asarray(bounds)
         self.start, self.stop = int(self.bounds[rank]), int(self.bounds[rank + 1])
         self.block_rows = int(np.diff(self.bounds).max()) if world > 0 else 0
@@ -113,6 +114,28 @@ class RowPartitionedCSR:
         self._gather_buf = {}
         if exchange == "halo":
             self.send_index = torch.as_tensor(self.send_index_host, device=self.device)
+
+    def resolve_mode(self, mode: str = "auto") -> str:
+        """One SpMM mode for every rank. 'auto' is resolved from ALL row blocks (every rank
+        holds the host indptr, so no communication): 'fast' if any block's longest row would
+        outlast its launch (sparse.auto_mode), else 'rowwise' if every block picks it, else
+        'ordered'. Every rank -- and every N of a scaling series whose blocks resolve alike --
+        then runs the same arithmetic; per-block choices are kept in `block_modes`."""
+        if mode != "auto":
+            return mode
+        from .sparse import auto_mode
+        ip = np.asarray(self._indptr_host, dtype=np.int64)
+        b = self.bounds
+        self.block_modes = []
+        for q in range(self.world):
+            lens = np.diff(ip[b[q]:b[q + 1] + 1])
+            self.block_modes.append(auto_mode(int(lens.size), int(lens.sum()),
+                                              int(lens.max()) if lens.size else 0))
+        if "fast" in self.block_modes:
+            return "fast"
+        if all(m == "rowwise" for m in self.block_modes):
+            return "rowwise"
+        return "ordered"
 
     @property
     def n_local_rows(self) -> int:

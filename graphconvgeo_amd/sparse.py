@@ -42,14 +42,19 @@ AUTO_ROWWISE_SKEW = 4
 AUTO_ROWWISE_MIN_ROWS = 65536
 
 
-def resolve_auto(A) -> str:
-    """The mode 'auto' runs on A: 'fast', 'rowwise' or 'ordered' (see above)."""
-    longest, nnz = A.max_row_nnz(), max(A.nnz, 1)
+def auto_mode(n_rows: int, nnz: int, longest: int) -> str:
+    """The mode 'auto' picks for a CSR of n_rows rows, nnz nonzeros and longest row `longest`."""
+    nnz = max(int(nnz), 1)
     if longest * AUTO_SPLIT_RATIO > nnz:
         return "fast"
-    if A.n_rows >= AUTO_ROWWISE_MIN_ROWS and longest * A.n_rows <= AUTO_ROWWISE_SKEW * nnz:
+    if n_rows >= AUTO_ROWWISE_MIN_ROWS and longest * n_rows <= AUTO_ROWWISE_SKEW * nnz:
         return "rowwise"
     return "ordered"
+
+
+def resolve_auto(A) -> str:
+    """The mode 'auto' runs on A: 'fast', 'rowwise' or 'ordered' (see above)."""
+    return auto_mode(A.n_rows, A.nnz, A.max_row_nnz())
 
 # DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
 # the dense MFMA GEMM -- break-even is ~1.5-2 % (a gathered nonzero ~190 ps, a dense element
