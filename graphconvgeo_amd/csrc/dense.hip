@@ -830,8 +830,13 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 // sets keeps PD steps of loads in flight. Partials [split][Mp][Np] are summed in split order
 // by gemm_tn_reduce_kernel (deterministic), which applies scale (a device scalar).
 // ---------------------------------------------------------------------------------------
-template <int MG, int NG, int PD>
-__global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
+// WM = 1: the workgroup's 4 waves sit side by side along N (tile 64*MG x 256*NG): they load
+// the same A rows, and each 64-row band of C re-reads B. WM > 1 (round 3): WM waves stacked
+// along M (tile 64*MG*WM x 64*NG, WM = 5 covers M = 300 in one tile): B -- the wide operand,
+// G at 840k x 930 -- is read once per row and shared by the WM waves through L1, and the N
+// tiles of one split (same XCD, remap) share A through L2.
+template <int MG, int NG, int PD, int WM = 1>
+__global__ __launch_bounds__(WM == 1 ? 256 : 64 * WM, 2) void gemm_tn_partial_kernel(
     int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt,
     int remap) {
@@ -848,9 +853,10 @@ __global__ __launch_bounds__(256, 2) void gemm_tn_partial_kernel(
     tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
   }
   const int bx = tile % mt, by = (tile / mt) % nt, bz = tile / (mt * nt);
-  const int m0 = bx * (64 * MG);
-  const int n0 = by * (256 * NG) + wave * (64 * NG);
-  if (n0 >= N) return;  // a wave wholly past N (no LDS, no barriers: safe to leave early)
+  const int m0 = WM == 1 ? bx * (64 * MG) : bx * (64 * MG * WM) + wave * (64 * MG);
+  const int n0 = WM == 1 ? by * (256 * NG) + wave * (64 * NG) : by * (64 * NG);
+  // a wave wholly past N (or M) leaves at once (no LDS, no barriers: safe)
+  if (n0 >= N || (WM > 1 && m0 >= M)) return;
   const int t_begin = bz * rows_per_split;
   const int t_end = min(R, t_begin + rows_per_split);
   const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
@@ -994,7 +1000,7 @@ __global__ __launch_bounds__(64 * kTnRedWaves) void gemm_tn_reduce_kernel(
 }
 
 struct TnPlan {
-  int mg, ng, pd;  // tile variant
+  int mg, ng, pd, wm = 1;  // tile variant (wm: waves stacked along M)
   int mt, nt, S, rows_per_split, Mp, Np;
 };
 
@@ -1004,12 +1010,12 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // columns and its waves past N leave at once, so N <= 512 runs more busy waves with NG = 1
   // (1.4M x 300 x 256: 2.49 vs 4.38 ms; x 930: NG = 2 87.7 vs 82.5 TFLOP/s)
   p.mg = 1, p.ng = N > 512 ? 2 : 1, p.pd = 8;
-  if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD"
-    int a = 0, b = 0, c = 0;
-    if (std::sscanf(v, "%d,%d,%d", &a, &b, &c) == 3) p.mg = a, p.ng = b, p.pd = c;
+  if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD[,WM]"
+    int a = 0, b = 0, c = 0, d = 1;
+    if (std::sscanf(v, "%d,%d,%d,%d", &a, &b, &c, &d) >= 3) p.mg = a, p.ng = b, p.pd = c, p.wm = d;
   }
-  p.mt = static_cast<int>((M + 64 * p.mg - 1) / (64 * p.mg));
-  p.nt = static_cast<int>((N + 256 * p.ng - 1) / (256 * p.ng));
+  p.mt = static_cast<int>((M + 64 * p.mg * p.wm - 1) / (64 * p.mg * p.wm));
+  p.nt = static_cast<int>((N + (p.wm == 1 ? 256 : 64) * p.ng - 1) / ((p.wm == 1 ? 256 : 64) * p.ng));
   // ~2 workgroups per CU-slot of the 256 CUs, at least 256 rows per split, 16-row aligned
   const int64_t want = std::max<int64_t>(1, 2048 / std::max(1, p.mt * p.nt));
   const int64_t max_s = std::max<int64_t>(1, R / 256);
@@ -1018,8 +1024,8 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   rps = (rps + 15) / 16 * 16;
   p.rows_per_split = static_cast<int>(std::max<int64_t>(rps, 16));
   p.S = static_cast<int>((R + p.rows_per_split - 1) / p.rows_per_split);
-  p.Mp = p.mt * 64 * p.mg;
-  p.Np = p.nt * 256 * p.ng;
+  p.Mp = p.mt * 64 * p.mg * p.wm;
+  p.Np = p.nt * (p.wm == 1 ? 256 : 64) * p.ng;
   return p;
 }
 
@@ -1424,16 +1430,20 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   const dim3 grid(static_cast<unsigned>(n_tiles));
   const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
   const int remap = rmv ? std::atoi(rmv) : 1;
-#define GCG_TN_CASE(MG_, NG_, PD_)                                                           \
-  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_) {                                           \
-    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_>), grid, dim3(256), 0, s, int(R),\
-                       int(M), int(N), A, lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np,   \
-                       p.mt, p.nt, remap);                                                   \
+#define GCG_TN_CASE(MG_, NG_, PD_, WM_)                                                      \
+  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_) {                            \
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_>), grid,                   \
+                       dim3(WM_ == 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
+                       B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);       \
   } else
-  GCG_TN_CASE(1, 2, 4)
-  GCG_TN_CASE(1, 2, 8)
-  GCG_TN_CASE(1, 1, 8)
-  GCG_TN_CASE(1, 1, 16)
+  GCG_TN_CASE(1, 2, 4, 1)
+  GCG_TN_CASE(1, 2, 8, 1)
+  GCG_TN_CASE(1, 1, 8, 1)
+  GCG_TN_CASE(1, 1, 16, 1)
+  GCG_TN_CASE(1, 2, 8, 4)
+  GCG_TN_CASE(1, 2, 8, 5)
+  GCG_TN_CASE(1, 1, 8, 4)
+  GCG_TN_CASE(1, 1, 8, 5)
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
 #undef GCG_TN_CASE
   GCG_HIP_CHECK(hipGetLastError());
