@@ -1010,6 +1010,11 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // columns and its waves past N leave at once, so N <= 512 runs more busy waves with NG = 1
   // (1.4M x 300 x 256: 2.49 vs 4.38 ms; x 930: NG = 2 87.7 vs 82.5 TFLOP/s)
   p.mg = 1, p.ng = N > 512 ? 2 : 1, p.pd = 8;
+  // M <= 256 in whole 64-row bands and N <= 512 (the X-head gradient G^T.Xh: 1.4M x 300 x 256
+  // as 300 x 256 with the roles below): M/64 waves stacked along M -- A (the narrow operand) is
+  // then split over the waves and B read once per row: 85-89 -> 112-115 TFLOP/s. Not for the
+  // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
+  if (M <= 256 && M % 64 == 0 && N <= 512) p.ng = 1, p.wm = static_cast<int>(M / 64);
   if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD[,WM]"
     int a = 0, b = 0, c = 0, d = 1;
     if (std::sscanf(v, "%d,%d,%d,%d", &a, &b, &c, &d) >= 3) p.mg = a, p.ng = b, p.pd = c, p.wm = d;
@@ -1442,6 +1447,8 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   GCG_TN_CASE(1, 1, 16, 1)
   GCG_TN_CASE(1, 2, 8, 4)
   GCG_TN_CASE(1, 2, 8, 5)
+  GCG_TN_CASE(1, 1, 8, 2)
+  GCG_TN_CASE(1, 1, 8, 3)
   GCG_TN_CASE(1, 1, 8, 4)
   GCG_TN_CASE(1, 1, 8, 5)
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }

@@ -393,17 +393,19 @@ class DeviceCSR:
         from . import dense
         cols, Xh, tail_t = split
         G = _check_dense(G, tail_t)
-        # the MFMA head product on a side stream, overlapping the HBM-bound tail gather;
-        # computed as (G^T . X_head)^T: K (300) x Fh (a multiple of 64) tiles the split-K
-        # kernel with no idle waves (2.5 ms vs 3.7 ms for X_head^T . G at Twitter-World)
+        # the MFMA head product X_head^T . G (Fh x K: Fh <= 256 in 64-row bands, so the
+        # split-K kernel stacks Fh/64 waves along it, round 3: 1.87 ms at Twitter-World, was
+        # 2.5 ms as (G^T . X_head)^T) on a side stream, overlapping the HBM-bound tail gather
         main = torch.cuda.current_stream(self.device)
         side = dense._side_stream(self.device) if TMATMUL_HEAD_SIDE_STREAM else main
         side.wait_stream(main)
         with torch.cuda.stream(side):
-            head_t = dense.gemm_tn(G, Xh)
+            G.record_stream(side)  # G (main-stream memory) is read on the side stream
+            head = dense.gemm_tn(Xh, G)
+            head.record_stream(main)  # side-stream memory, read by the index_copy below
         out = spmm(tail_t, G, mode=mode, out=out)
         main.wait_stream(side)
-        out.index_copy_(0, cols, head_t.t())
+        out.index_copy_(0, cols, head)
         return out
 
     def __repr__(self):

@@ -332,8 +332,9 @@ def test_ordered_cooperative_world_scale_block(cuda):
     n = H.shape[0]
     Z = dense(n, 300)
     A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
-    assert A.plan(None, True, 0).info()["n_long_rows"] > 0
-    Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered").cpu().numpy()
+    # 128-nnz tasks: rows over 1024 nonzeros (hub rows up to 0.01 N = 2000) go cooperative
+    assert A.plan(None, True, 128).info()["n_long_rows"] > 0
+    Y = gs.spmm(A, to_dev(Z, cuda), mode="ordered", task_nnz=128).cpu().numpy()
     lens = np.diff(H.indptr)
     hubs = np.argsort(lens)[-64:]
     sample = np.unique(np.concatenate([hubs, np.random.default_rng(0).choice(n, 2000)]))
