@@ -66,6 +66,38 @@ __device__ __forceinline__ int reduce16_min(int v) {
 
 constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 
+// Reductions over the 16 lanes of a DPP row (lanes 16q .. 16q + 15: one output row of the
+// MFMA layout) with DPP lane swaps -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
+// row_mirror -- instead of ds_bpermute shuffles. Every lane of the row ends with the same
+// value (each step combines a and b as op(a, b) in one lane and op(b, a) in its partner).
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
+                                                            0xF, 0xF, false));
+}
+template <int CTRL>
+__device__ __forceinline__ int dpp_i(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float row16_max(float v) {
+  v = fmaxf(v, dpp_f<0xB1>(v));
+  v = fmaxf(v, dpp_f<0x4E>(v));
+  v = fmaxf(v, dpp_f<0x141>(v));
+  return fmaxf(v, dpp_f<0x140>(v));
+}
+__device__ __forceinline__ float row16_sum(float v) {
+  v = v + dpp_f<0xB1>(v);
+  v = v + dpp_f<0x4E>(v);
+  v = v + dpp_f<0x141>(v);
+  return v + dpp_f<0x140>(v);
+}
+__device__ __forceinline__ int row16_min(int v) {
+  v = min(v, dpp_i<0xB1>(v));
+  v = min(v, dpp_i<0x4E>(v));
+  v = min(v, dpp_i<0x141>(v));
+  return min(v, dpp_i<0x140>(v));
+}
+
 
 template <int RT, int G, int WR, int WC, int EPI, int PF>
 __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) void gemm_kernel(
@@ -220,7 +252,8 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   if constexpr (EPI == 1) {
     for (int c = tid; c < BN; c += NT) {
       const int gc = blockIdx.y * BN + c;
-      sbias[c] = (bias != nullptr && gc < N) ? bias[gc] : 0.f;
+      // columns past N: -inf, so their softmax weight is exactly 0 (no mask in the epilogue)
+      sbias[c] = gc < N ? (bias != nullptr ? bias[gc] : 0.f) : kNegInf;
     }
     for (int r = tid; r < BM; r += NT) {
       const int64_t row = row0 + r;

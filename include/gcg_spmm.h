@@ -91,7 +91,9 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
  * reused for every K. Reads indptr (and out_rows) back to the host once and
  * validates indptr; this call synchronizes `stream` -- it is NOT a hot-path call.
  *   task_nnz  : target nonzeros per wave task (0 = default: clamp(nnz / 8192, 32, 512)).
- *   ordered   : 1 = never split a row (bitwise scipy order, long rows serial);
+ *   ordered   : 1 = never split a row (bitwise scipy order): rows longer than task_nnz are
+ *                   scheduled first, those longer than 8 x task_nnz on a whole workgroup each
+ *                   (the storage-order sum handed from wave to wave, still bitwise);
  *               0 = split rows longer than task_nnz into segments (fast).
  */
 typedef struct gcg_spmm_plan gcg_spmm_plan;
@@ -103,7 +105,8 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
 gcg_status gcg_spmm_plan_destroy(gcg_spmm_plan* plan);
 /* Bytes of device workspace gcg_spmm_csr_f32_planned needs for width K (0 if none). */
 gcg_status gcg_spmm_plan_workspace_bytes(const gcg_spmm_plan* plan, int64_t K, size_t* bytes);
-/* Plan statistics: wave tasks, rows split into segments, segments, max task nnz. */
+/* Plan statistics: tasks, long rows (split into segments in a fast plan, run on a whole
+ * workgroup in an ordered plan), segments, max task nnz. */
 gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64_t* n_long_rows,
                               int64_t* n_segments, int64_t* max_task_nnz);
 
@@ -338,6 +341,8 @@ gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
  *   out may be NULL when labels are given (evaluation: loss and accuracy only).
  * scale_dev (nullable, device): multiplies scale (the upstream gradient of the loss, read
  * on the device so the call can sit inside a captured HIP graph). The logits never reach HBM.
+ * out needs ldo % 4 == 0 and a 16-B aligned base; its padding columns [N, round4(N)) are
+ * written with zeros (whole dwordx4 row stores).
  */
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
                                         int64_t lda, const float* W, int64_t ldw,
