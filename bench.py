@@ -145,7 +145,7 @@ def cpu_multicore(H, K: int, budget_s: float) -> dict:
             "sample": f"rows [0, {blk.shape[0]}): {blk.nnz} nnz x K={K}, {reps} reps"}
 
 
-PROFILE_ROUNDS = ("r02", "r01")  # newest first
+PROFILE_ROUNDS = ("r03", "r02", "r01")  # newest first
 
 
 def load_traffic(workload: str, per_launch_bytes: int):
