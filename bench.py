@@ -389,7 +389,9 @@ def main():
     ap.add_argument("--no-dense", dest="dense", action="store_false",
                     help="N = 1: skip timing the output layer's MFMA kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--chunks", type=int, default=2,
+    # 4 chunks: every N > 1 step is exchange-bound on xGMI, so the exposed
+    # time is ~ exchange + SpMM/chunks x the chunking cost (x1.06 at 2 chunks, x1.26-1.30 at 4)
+    ap.add_argument("--chunks", type=int, default=4,
                     help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
     ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "halo"],
                     help="N > 1: all-gather every block, or send only the referenced halo rows")
