@@ -42,6 +42,10 @@ def test_bench_single_gpu_line(cuda):
     rf = rec["roofline"]
     assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["frac_vs_achievable"] > 0
     assert rec["variants"]["uniform"]["kernel_ms"] > 0 and rec["variants"]["k1500"]["kernel_ms"] > 0
+    # the like-for-like point of the scaling series: the same SpMM in the mode N > 1 runs
+    if not rec["config"]["mode"].endswith("fast"):
+        assert rec["variants"]["fast"]["mode"] == "fast" and rec["variants"]["fast"]["kernel_ms"] > 0
+    assert "mode_resolution" in rec["config"]
     dk = {k: v for k, v in rec["dense_kernels"].items() if isinstance(v, dict)}
     assert len(dk) == 4 and all(v["TFLOPs"] > 0 and v["frac"] < 1 for v in dk.values())
 
@@ -56,6 +60,9 @@ def test_bench_two_ranks_gloo(cuda):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "row2"
+    # one mode for every rank, resolved over all row blocks
+    assert rec["config"]["mode_resolution"].startswith("global over the row blocks")
+    assert rec["config"]["mode"].split("->")[1] in ("fast", "ordered", "rowwise")
     d = rec["distributed"]
     assert d["world_size"] == 2 and d["backend"] == "gloo"
     for key in ("exchange", "exchange_ms", "local_spmm_ms", "comm_fraction"):
