@@ -452,7 +452,7 @@ def main():
         part = RowPartitionedCSR(H, rank, world, dev, exchange=args.exchange)
         Zl = torch.randn((part.local_block_rows, K), generator=gen, device=dev, dtype=torch.float32)
         Y = gs.empty_dense(part.n_local, K, dev)
-        # one mode for every rank, resolved from all row blocks (RowPartitionedCSR.resolve_mode)
+        # one mode for every rank and every N: the whole graph's (RowPartitionedCSR.resolve_mode)
         eff = part.resolve_mode(args.mode)
         part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
         info = part.A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
@@ -585,7 +585,8 @@ def main():
         "edges_per_s": round(nnz / (ms * 1e-3)),
         "config": {"workload": f"{cfg.name} H.Z SpMM fwd, {args.graph} degrees", "nodes": N,
                    "edges": cfg.n_edges, "nnz_H": nnz, "K": K, "mode": f"{args.mode}->{eff}",
-                   "mode_resolution": ("global over the row blocks: " + ",".join(
+                   "mode_resolution": ("the whole graph (RowPartitionedCSR.resolve_mode), the "
+                                       "same at every N; each row block alone: " + ",".join(
                        getattr(part, "block_modes", [])) if (world > 1 or args.partitioned)
                                        else "the whole graph (sparse.resolve_auto)"),
                    "parallelism": f"row{world}" if world > 1 else "single",
@@ -606,9 +607,9 @@ def main():
             rec["variants"]["k1500"] = spmm_wide_variant(A, N, nnz, 1500, eff,
                                                          max(args.steps // 4, 3), dev)
         if eff != "fast":
-            # the same SpMM in 'fast' mode (hub rows split, within 1e-5): the arithmetic the
-            # N > 1 lines run when a row block's hub rows force it (RowPartitionedCSR.resolve_mode),
-            # so the scaling series has a like-for-like N = 1 point
+            # the same SpMM in 'fast' mode (hub rows split, within 1e-5): the N = 1 point of a
+            # `--mode fast` scaling series (the default series runs the whole graph's mode,
+            # 'ordered', at every N: RowPartitionedCSR.resolve_mode)
             rec["variants"]["fast"] = spmm_mode_variant(A, H, K, "fast", max(args.steps, 5), dev)
     if world == 1 and not args.partitioned and args.dense:
         rec["dense_kernels"] = dense_kernels_bench(max(args.steps // 2, 5), dev)

@@ -173,6 +173,7 @@ class RowPartitionedGCN:
         self.regul_coefs = tuple(regul_coefs)
         H = sps.csr_matrix(H)
         self.part = RowPartitionedCSR(H, rank, world, self.device, group=group, exchange=exchange)
+        self.mode = self.part.resolve_mode(mode)  # one SpMM mode on every rank (the whole graph's)
         start, stop = self.part.start, self.part.stop
         Xc = sps.csr_matrix(X)[start:stop]
         self.X_p = gs.DeviceCSR.from_scipy(Xc, self.device)

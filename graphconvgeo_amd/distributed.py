@@ -116,13 +116,14 @@ class RowPartitionedCSR:
             self.send_index = torch.as_tensor(self.send_index_host, device=self.device)
 
     def resolve_mode(self, mode: str = "auto") -> str:
-        """One SpMM mode for every rank. 'auto' is resolved from ALL row blocks (every rank
-        holds the host indptr, so no communication): 'fast' if any block's longest row would
-        outlast its launch (sparse.auto_mode), else 'rowwise' if every block picks it, else
-        'ordered'. Every rank -- and every N of a scaling series whose blocks resolve alike --
-        then runs the same arithmetic; per-block choices are kept in `block_modes`."""
-        if mode != "auto":
-            return mode
+        """One SpMM mode for every rank and every N: 'auto' is resolved from the WHOLE graph
+        (sparse.auto_mode on the global indptr, which every rank holds: no communication), the
+        choice the unpartitioned N = 1 SpMM makes -- so a scaling series runs the same
+        arithmetic at every N ('ordered' on the World graph: bitwise scipy at every N). What
+        each row block alone would pick is kept in `block_modes` (reporting): at N >= 2 the
+        World blocks would pick 'fast' for their ~12k-nonzero hub rows, which the ordered plan
+        runs on whole workgroups instead (spmm.hip coop_row; at P = 8 1.16 ms vs 0.91 ms
+        fast, against an exchange of several ms)."""
         from .sparse import auto_mode
         ip = np.asarray(self._indptr_host, dtype=np.int64)
         b = self.bounds
@@ -131,11 +132,10 @@ class RowPartitionedCSR:
             lens = np.diff(ip[b[q]:b[q + 1] + 1])
             self.block_modes.append(auto_mode(int(lens.size), int(lens.sum()),
                                               int(lens.max()) if lens.size else 0))
-        if "fast" in self.block_modes:
-            return "fast"
-        if all(m == "rowwise" for m in self.block_modes):
-            return "rowwise"
-        return "ordered"
+        if mode != "auto":
+            return mode
+        lens = np.diff(ip)
+        return auto_mode(int(lens.size), int(ip[-1]), int(lens.max()) if lens.size else 0)
 
     @property
     def n_local_rows(self) -> int:

@@ -60,8 +60,8 @@ def test_bench_two_ranks_gloo(cuda):
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "row2"
-    # one mode for every rank, resolved over all row blocks
-    assert rec["config"]["mode_resolution"].startswith("global over the row blocks")
+    # one mode for every rank and every N: the whole graph's
+    assert rec["config"]["mode_resolution"].startswith("the whole graph")
     assert rec["config"]["mode"].split("->")[1] in ("fast", "ordered", "rowwise")
     d = rec["distributed"]
     assert d["world_size"] == 2 and d["backend"] == "gloo"

@@ -349,24 +349,24 @@ def test_row_partitioned_fit_loop_and_gather():
 
 
 def test_mode_resolved_once_for_all_ranks():
-    """'auto' at N > 1 is one mode for every rank, resolved from every row block on the host
-    (RowPartitionedCSR.resolve_mode): 'fast' as soon as one block's hub row would outlast its
-    launch, the same answer on every rank; explicit modes pass through."""
+    """'auto' at N > 1 is the mode the whole graph resolves to (RowPartitionedCSR.resolve_mode),
+    the same on every rank and at every N, so a scaling series runs one arithmetic; what each
+    row block alone would pick is reported in block_modes; explicit modes pass through."""
     from graphconvgeo_amd import sparse as gs
     from graphconvgeo_amd.distributed import RowPartitionedCSR
     H = synthetic_graph(60_000, 600_000)  # power-law: hub rows
     lens = np.diff(H.indptr)
-    assert gs.auto_mode(H.shape[0], H.nnz, int(lens.max())) in ("ordered", "fast")
-    got = []
-    for r in range(4):
-        part = RowPartitionedCSR(H, r, 4, "cpu", local_spmm=_oracle_spmm, exchange="allgather")
-        got.append((part.resolve_mode("auto"), tuple(part.block_modes)))
-        assert part.resolve_mode("ordered") == "ordered"
-    assert len(set(got)) == 1  # every rank the same mode and the same per-block view
-    mode, blocks = got[0]
-    assert mode == ("fast" if "fast" in blocks else
-                    "rowwise" if set(blocks) == {"rowwise"} else "ordered")
-    for q, m in enumerate(blocks):
-        b = RowPartitionedCSR(H, q, 4, "cpu", local_spmm=_oracle_spmm).bounds
-        L = lens[b[q]:b[q + 1]]
-        assert m == gs.auto_mode(L.size, int(L.sum()), int(L.max()))
+    whole = gs.auto_mode(H.shape[0], H.nnz, int(lens.max()))
+    for P in (2, 4):
+        got = []
+        for r in range(P):
+            part = RowPartitionedCSR(H, r, P, "cpu", local_spmm=_oracle_spmm, exchange="allgather")
+            got.append((part.resolve_mode("auto"), tuple(part.block_modes)))
+            assert part.resolve_mode("fast") == "fast"
+        assert len(set(got)) == 1  # every rank the same mode and the same per-block view
+        mode, blocks = got[0]
+        assert mode == whole and len(blocks) == P
+        for q, m in enumerate(blocks):
+            b = RowPartitionedCSR(H, q, P, "cpu", local_spmm=_oracle_spmm).bounds
+            L = lens[b[q]:b[q + 1]]
+            assert m == gs.auto_mode(L.size, int(L.sum()), int(L.max()))
