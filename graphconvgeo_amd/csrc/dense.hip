@@ -201,17 +201,27 @@ __global__ __launch_bounds__(64 * WR * WC, (PF == 1 && WR * WC == 4) ? 1 : 2) vo
   // ---- B fragments for one 16-deep k-step: bf[g][e] = B[k0 + 4q + e][bcol[g] .. +3] ----
   // Fragments (g, e) with unit u = 4g + e in [u0, u1) only (the split ping-pong body loads
   // one part of the set at a time).
-  auto load_b = [&](f4 (&bf)[G][4], int k0, int u0 = 0, int u1 = 4 * G) {
+  // B is read through a buffer descriptor re-based at row k0 for every step (scalar work): the
+  // range check returns 0 for rows past K (A is 0 there as well), so the per-lane row clamp and
+  // 64-bit row addresses of round 2 (~48 VALU per 16-deep step, VALU that lowered the clock this
+  // MFMA loop holds) are gone; the per-lane byte offsets are constants. Host: K * ldb * 4 < 2^31.
+  uint32_t boff[G][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      int k = k0 + 4 * q + e;
-      k = k < K ? k : K - 1;  // A is zero there; any finite B row does
-      const float* brow = B + static_cast<int64_t>(k) * ldb;
+  for (int g = 0; g < G; ++g)
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+      boff[g][e] = static_cast<uint32_t>(((4 * q + e) * static_cast<int>(ldb) + bcol[g]) * 4);
+  auto load_b = [&](f4 (&bf)[G][4], int k0, int u0 = 0, int u1 = 4 * G) {
+    const int kb = k0 < K ? k0 : K;  // a prefetch past K gets an empty range: zeros
+    const auto rs = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(B + static_cast<int64_t>(kb) * ldb), static_cast<short>(0),
+        (K - kb) * static_cast<int>(ldb) * 4, 0x00020000);
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
 #pragma unroll
       for (int g = 0; g < G; ++g)
         if (4 * g + e >= u0 && 4 * g + e < u1)
-          bf[g][e] = *reinterpret_cast<const f4*>(brow + bcol[g]);
-    }
+          bf[g][e] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rs, boff[g][e], 0, 0));
   };
 
   const int arow = wr * 16 * RT + j;
@@ -868,8 +878,13 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 // along M (tile 64*MG*WM x 64*NG, WM = 5 covers M = 300 in one tile): B -- the wide operand,
 // G at 840k x 930 -- is read once per row and shared by the WM waves through L1, and the N
 // tiles of one split (same XCD, remap) share A through L2.
+// WM = 0 (round 3): every wave owns its own 64*MG x 64*NG tile, enumerated m fastest over
+// (m tile, n tile, split), 4 consecutive wave tiles per workgroup (the 4 waves of a workgroup
+// then share their B rows through L1), one wave per SIMD: the accumulators of a wide NG (3 or
+// 5: N = 930 in 960 columns instead of the 1024 of 256-column workgroup tiles) live in the
+// 512-register file beside a deep load ring.
 template <int MG, int NG, int PD, int WM = 1>
-__global__ __launch_bounds__(WM == 1 ? 256 : 64 * WM, 2) void gemm_tn_partial_kernel(
+__global__ __launch_bounds__(WM <= 1 ? 256 : 64 * WM, WM == 0 ? 1 : 2) void gemm_tn_partial_kernel(
     int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt,
     int remap) {
@@ -885,11 +900,17 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 64 * WM, 2) void gemm_tn_partial_ke
     const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
     tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
   }
-  const int bx = tile % mt, by = (tile / mt) % nt, bz = tile / (mt * nt);
-  const int m0 = WM == 1 ? bx * (64 * MG) : bx * (64 * MG * WM) + wave * (64 * MG);
-  const int n0 = WM == 1 ? by * (256 * NG) + wave * (64 * NG) : by * (64 * NG);
-  // a wave wholly past N (or M) leaves at once (no LDS, no barriers: safe)
-  if (n0 >= N || (WM > 1 && m0 >= M)) return;
+  const int wt = WM == 0 ? 4 * tile + wave : tile;  // WM = 0: the wave's own tile
+  const int bx = wt % mt, by = (wt / mt) % nt, bz = wt / (mt * nt);
+  const int m0 = WM == 0   ? bx * (64 * MG)
+                 : WM == 1 ? bx * (64 * MG)
+                           : bx * (64 * MG * WM) + wave * (64 * MG);
+  const int n0 = WM == 0   ? by * (64 * NG)
+                 : WM == 1 ? by * (256 * NG) + wave * (64 * NG)
+                           : by * (64 * NG);
+  // a wave wholly past N (or M), or past the last split, leaves at once (no LDS, no barriers)
+  if (n0 >= N || (WM != 1 && m0 >= M)) return;
+  if (static_cast<int64_t>(bz) * rows_per_split >= R) return;
   const int t_begin = bz * rows_per_split;
   const int t_end = min(R, t_begin + rows_per_split);
   const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
@@ -915,26 +936,33 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 64 * WM, 2) void gemm_tn_partial_ke
         for (int eb = 0; eb < 4; ++eb) acc[a][b][ea][eb] = f4{0.f, 0.f, 0.f, 0.f};
 
   f4 ra[PD][MG], rb[PD][NG];
-  bool rok[PD];
+  // A and B rows through buffer descriptors re-based at the step's first row (scalar work): the
+  // range check covers only the rows left in the split, so rows past it read as 0 -- no per-lane
+  // row clamp, select or 64-bit address arithmetic (round 3; the per-lane byte offsets are
+  // constants). Host: lda, ldb < 2^27.
+  uint32_t aoff[MG], boff[NG];
+#pragma unroll
+  for (int g = 0; g < MG; ++g) aoff[g] = static_cast<uint32_t>((q * static_cast<int>(lda) + acol[g]) * 4);
+#pragma unroll
+  for (int g = 0; g < NG; ++g) boff[g] = static_cast<uint32_t>((q * static_cast<int>(ldb) + bcol[g]) * 4);
   auto load = [&](int u, int t0) {
-    const int t = t0 + q;
-    const bool ok = t < t_end;
-    const int tc = ok ? t : t_begin;  // clamped row, zeroed at use
-    const float* arow = A + static_cast<int64_t>(tc) * lda;
-    const float* brow = B + static_cast<int64_t>(tc) * ldb;
-    rok[u] = ok;
+    // (readfirstlane: the descriptor must be provably wave-uniform, or hipcc emits a waterfall)
+    const int left = __builtin_amdgcn_readfirstlane(min(max(t_end - t0, 0), 4));  // rows in split
+    const int tb = __builtin_amdgcn_readfirstlane(left > 0 ? t0 : t_begin);
+    const auto ar = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(A + static_cast<int64_t>(tb) * lda), static_cast<short>(0),
+        left * static_cast<int>(lda) * 4, 0x00020000);
+    const auto br = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<float*>(B + static_cast<int64_t>(tb) * ldb), static_cast<short>(0),
+        left * static_cast<int>(ldb) * 4, 0x00020000);
 #pragma unroll
-    for (int g = 0; g < MG; ++g) ra[u][g] = *reinterpret_cast<const f4*>(arow + acol[g]);
+    for (int g = 0; g < MG; ++g)
+      ra[u][g] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff[g], 0, 0));
 #pragma unroll
-    for (int g = 0; g < NG; ++g) rb[u][g] = *reinterpret_cast<const f4*>(brow + bcol[g]);
+    for (int g = 0; g < NG; ++g)
+      rb[u][g] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(br, boff[g], 0, 0));
   };
   auto compute = [&](int u) {
-    // Rows past the split are zeroed here, at use, not at load: a select right after the load
-    // makes hipcc wait for it there, draining the PD-deep ring every step (round 2: ISA showed
-    // vmcnt(0)/(1) before every step's MFMAs).
-    f4 av[MG];
-#pragma unroll
-    for (int a = 0; a < MG; ++a) av[a] = rok[u] ? ra[u][a] : f4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int a = 0; a < MG; ++a)
 #pragma unroll
@@ -943,7 +971,7 @@ __global__ __launch_bounds__(WM == 1 ? 256 : 64 * WM, 2) void gemm_tn_partial_ke
         for (int ea = 0; ea < 4; ++ea)
 #pragma unroll
           for (int eb = 0; eb < 4; ++eb)
-            acc[a][b][ea][eb] = mfma4(av[a][ea], rb[u][b][eb], acc[a][b][ea][eb]);
+            acc[a][b][ea][eb] = mfma4(ra[u][a][ea], rb[u][b][eb], acc[a][b][ea][eb]);
   };
   // steps of 4 rows; the ring is refilled PD steps ahead (loads past t_end are zeroed)
 #pragma unroll
@@ -1039,10 +1067,16 @@ struct TnPlan {
 
 TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   TnPlan p;
-  // NG = 2 (4 + 4 dwordx4 loads feed 32 MFMAs) unless N is narrow: a workgroup spans 256*NG
-  // columns and its waves past N leave at once, so N <= 512 runs more busy waves with NG = 1
-  // (1.4M x 300 x 256: 2.49 vs 4.38 ms; x 930: NG = 2 87.7 vs 82.5 TFLOP/s)
-  p.mg = 1, p.ng = N > 512 ? 2 : 1, p.pd = 8;
+  // Default: per-wave 64 x 64*NG tiles (WM = 0), NG = 3 or 2, whichever pads N less (ties: 3,
+  // fewer loads per MFMA). The round-2 workgroup tiles (WM = 1: 4 waves side by side, 64 x
+  // 256*NG) padded N = 930 to 1024 columns -- 15 % of the MFMAs computed discarded columns.
+  // World dW2 840k x 300 x 930: 960 padded columns, 105.8 -> 121.7 TFLOP/s; US dW2 270k x 300
+  // x 256 (NG = 2): 87-103 -> 118 (tools/exp_tn_wave.py).
+  p.mg = 1, p.pd = 8;
+  {
+    const int64_t pad3 = (N + 191) / 192 * 192, pad2 = (N + 127) / 128 * 128;
+    p.wm = 0, p.ng = pad3 <= pad2 ? 3 : 2;
+  }
   // M <= 256 in whole 64-row bands and N <= 512 (the X-head gradient G^T.Xh: 1.4M x 300 x 256
   // as 300 x 256 with the roles below): M/64 waves stacked along M -- A (the narrow operand) is
   // then split over the waves and B read once per row: 85-89 -> 112-115 TFLOP/s. Not for the
@@ -1052,18 +1086,24 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
     int a = 0, b = 0, c = 0, d = 1;
     if (std::sscanf(v, "%d,%d,%d,%d", &a, &b, &c, &d) >= 3) p.mg = a, p.ng = b, p.pd = c, p.wm = d;
   }
-  p.mt = static_cast<int>((M + 64 * p.mg * p.wm - 1) / (64 * p.mg * p.wm));
-  p.nt = static_cast<int>((N + (p.wm == 1 ? 256 : 64) * p.ng - 1) / ((p.wm == 1 ? 256 : 64) * p.ng));
-  // ~2 workgroups per CU-slot of the 256 CUs, at least 256 rows per split, 16-row aligned
-  const int64_t want = std::max<int64_t>(1, 2048 / std::max(1, p.mt * p.nt));
+  const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
+  const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
+  p.mt = static_cast<int>((M + tm - 1) / tm);
+  p.nt = static_cast<int>((N + tn - 1) / tn);
+  // ~2048 tiles: 2 workgroups per CU of the 256 CUs (WM = 0: the tiles are waves, 1 per SIMD,
+  // so 2 rounds of the 1024 SIMDs -- 1 round measured the same speed with 2x longer serial
+  // sums), at least 256 rows per split, 16-row aligned
+  int64_t slots = 2048;
+  if (const char* v = std::getenv("GCG_TN_SLOTS")) slots = std::max(1, std::atoi(v));  // knob
+  const int64_t want = std::max<int64_t>(1, slots / std::max(1, p.mt * p.nt));
   const int64_t max_s = std::max<int64_t>(1, R / 256);
   p.S = static_cast<int>(std::min(want, max_s));
   int64_t rps = (R + p.S - 1) / p.S;
   rps = (rps + 15) / 16 * 16;
   p.rows_per_split = static_cast<int>(std::max<int64_t>(rps, 16));
   p.S = static_cast<int>((R + p.rows_per_split - 1) / p.rows_per_split);
-  p.Mp = p.mt * 64 * p.mg * p.wm;
-  p.Np = p.nt * (p.wm == 1 ? 256 : 64) * p.ng;
+  p.Mp = p.mt * tm;
+  p.Np = p.nt * tn;
   return p;
 }
 
@@ -1223,6 +1263,10 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
     return fail(GCG_ERR_MISALIGNED, "%s: row_weight not 4-B aligned", fn);
   if (M == 0) return GCG_OK;
   const Shape sh = pick_shape(N, fused);
+  // gemm_kernel reads B through a 32-bit buffer range (K * ldb * 4 bytes)
+  if (!sh.BL && K * ldb * 4 >= (int64_t{1} << 31))
+    return fail(GCG_ERR_INVALID_ARG, "%s: B of %lld x %lld floats exceeds the 2 GB buffer range", fn,
+                static_cast<long long>(K), static_cast<long long>(ldb));
   dim3 grid(static_cast<unsigned>((M + sh.bm() - 1) / sh.bm()),
             static_cast<unsigned>((N + sh.bn() - 1) / sh.bn()));
   if (grid.x > 0x7fffffffu) return fail(GCG_ERR_INVALID_ARG, "%s: M too large", fn);
@@ -1450,6 +1494,8 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   if ((st = check_dense(fn, A, lda, (M + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
   if ((st = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
   if ((st = check_dense(fn, C, ldc, N, false)) != GCG_OK) return st;
+  if (lda >= (int64_t{1} << 27) || ldb >= (int64_t{1} << 27))  // 4-row buffer ranges < 2 GB
+    return fail(GCG_ERR_INVALID_ARG, "%s: leading dimension too large", fn);
   auto s = static_cast<hipStream_t>(stream);
   if (R == 0) {
     for (int64_t m = 0; m < M; ++m)
@@ -1463,15 +1509,16 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
                 need);
   if (!aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace not 16-B aligned", fn);
   float* part = static_cast<float*>(workspace);
-  const int64_t n_tiles = int64_t{p.mt} * p.nt * p.S;
+  int64_t n_tiles = int64_t{p.mt} * p.nt * p.S;
   if (n_tiles > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "%s: too many tiles", fn);
+  if (p.wm == 0) n_tiles = (n_tiles + 3) / 4;  // 4 wave tiles per workgroup
   const dim3 grid(static_cast<unsigned>(n_tiles));
   const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
   const int remap = rmv ? std::atoi(rmv) : 1;
 #define GCG_TN_CASE(MG_, NG_, PD_, WM_)                                                      \
   if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_) {                            \
     hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_>), grid,                   \
-                       dim3(WM_ == 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
+                       dim3(WM_ <= 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
                        B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);       \
   } else
   GCG_TN_CASE(1, 2, 4, 1)
@@ -1484,6 +1531,10 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   GCG_TN_CASE(1, 1, 8, 3)
   GCG_TN_CASE(1, 1, 8, 4)
   GCG_TN_CASE(1, 1, 8, 5)
+  GCG_TN_CASE(1, 2, 8, 0)
+  GCG_TN_CASE(1, 3, 8, 0)
+  GCG_TN_CASE(1, 3, 12, 0)
+  GCG_TN_CASE(1, 3, 6, 0)
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
 #undef GCG_TN_CASE
   GCG_HIP_CHECK(hipGetLastError());

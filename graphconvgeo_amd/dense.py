@@ -415,7 +415,7 @@ class _ProjectXent(torch.autograd.Function):
 
     Forward: one fused MFMA launch writes G = (softmax - onehot)/M (the logits gradient),
     per-row losses and hits; no logits in HBM. Backward (upstream g, a device scalar):
-    dP = G . (g W)^T (hipBLASLt), dW = g P^T . G (split-K MFMA gemm_tn), db = g colsum(G)."""
+    dP = G . (g W)^T (NT MFMA gemm_nt), dW = g P^T . G (split-K MFMA gemm_tn), db = g colsum(G)."""
 
     @staticmethod
     def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None, slot=None,

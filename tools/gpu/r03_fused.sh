@@ -1,0 +1,10 @@
+#!/bin/bash
+# Round 3: fused output layer A/B (wave rotation; buffer-descriptor B loads) + the dense GPU tests.
+set -o pipefail
+cd "$GRAFT_REPO_ROOT"
+out=gpurun_out/r03
+mkdir -p $out
+timeout -k 10 300 python -u tools/exp_fused_rot.py > $out/fused_rot.log 2>&1 || { tail -10 $out/fused_rot.log; exit 1; }
+cut -c1-600 $out/fused_rot.log
+timeout -k 10 600 python -u -m pytest -x -q --tb=short --timeout 300 --timeout-method thread -m gpu tests/test_dense_gpu.py tests/test_mlpconv_gpu.py tests/test_config3_gpu.py tests/test_ops_gpu.py > $out/dense_tests.log 2>&1 || { grep -E 'Error|assert|FAILED|passed|failed' $out/dense_tests.log | cut -c1-300 | tail -30; exit 1; }
+tail -2 $out/dense_tests.log
