@@ -209,6 +209,20 @@ def test_gemm_tn_vs_float64(cuda, R, M, N):
     assert np.array_equal(C3, (C * np.float32(2.5)))
 
 
+@pytest.mark.parametrize("layout", ["1,2,8,1", "1,3,8,0", "1,2,8,0", "1,3,12,0", "1,1,8,4"])
+@pytest.mark.parametrize("R,M,N", [(4097, 300, 930), (70001, 256, 300), (513, 70, 129), (5, 3, 200)])
+def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, layout, monkeypatch):
+    """Every split-K wave layout (GCG_TN=MG,NG,PD,WM: workgroup tiles WM = 1, per-wave tiles
+    WM = 0 -- the default -- and waves stacked along M) against float64, with ragged R (steps
+    that end inside a split read zeros through the buffer range check), M and N off the tiles."""
+    monkeypatch.setenv("GCG_TN", layout)
+    A, B = _rand((R, M), 45, 0.5), _rand((R, N), 46, 0.5)
+    At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
+    C = dense.gemm_tn(At, Bt).cpu().numpy()
+    _check_gemm(C, A.T.copy(), B)
+    assert np.array_equal(C, dense.gemm_tn(At, Bt).cpu().numpy())  # deterministic
+
+
 def test_gemm_tn_strided_views(cuda):
     R, M, N = 3000, 300, 930
     A, B = _rand((R, M), 43), _rand((R, N), 44)
