@@ -883,8 +883,10 @@ __global__ __launch_bounds__(256) void softmax_xent_rows_kernel(
 // then share their B rows through L1), one wave per SIMD: the accumulators of a wide NG (3 or
 // 5: N = 930 in 960 columns instead of the 1024 of 256-column workgroup tiles) live in the
 // 512-register file beside a deep load ring.
-template <int MG, int NG, int PD, int WM = 1>
-__global__ __launch_bounds__(WM <= 1 ? 256 : 64 * WM, WM == 0 ? 1 : 2) void gemm_tn_partial_kernel(
+// OCC = 2 keeps a per-wave (WM = 0) tile at 2 waves per SIMD (<= 256 registers: a shallow ring),
+// so it can share CUs with kernels running beside it on other streams.
+template <int MG, int NG, int PD, int WM = 1, int OCC = 0>
+__global__ __launch_bounds__(WM <= 1 ? 256 : 64 * WM, (WM == 0 && OCC != 2) ? 1 : 2) void gemm_tn_partial_kernel(
     int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt,
     int remap) {
@@ -1061,7 +1063,7 @@ __global__ __launch_bounds__(64 * kTnRedWaves) void gemm_tn_reduce_kernel(
 }
 
 struct TnPlan {
-  int mg, ng, pd, wm = 1;  // tile variant (wm: waves stacked along M)
+  int mg, ng, pd, wm = 1, occ = 0;  // tile variant (wm: waves stacked along M; occ: see kernel)
   int mt, nt, S, rows_per_split, Mp, Np;
 };
 
@@ -1081,10 +1083,13 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // as 300 x 256 with the roles below): M/64 waves stacked along M -- A (the narrow operand) is
   // then split over the waves and B read once per row: 85-89 -> 112-115 TFLOP/s. Not for the
   // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
-  if (M <= 256 && M % 64 == 0 && N <= 512) p.ng = 1, p.wm = static_cast<int>(M / 64);
-  if (const char* v = std::getenv("GCG_TN")) {  // experiment knob: "MG,NG,PD[,WM]"
-    int a = 0, b = 0, c = 0, d = 1;
-    if (std::sscanf(v, "%d,%d,%d,%d", &a, &b, &c, &d) >= 3) p.mg = a, p.ng = b, p.pd = c, p.wm = d;
+  const bool stacked = M <= 256 && M % 64 == 0 && N <= 512;
+  if (stacked) p.ng = 1, p.wm = static_cast<int>(M / 64);
+  // experiment knob: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes alone)
+  if (const char* v = std::getenv("GCG_TN"); v && !(stacked && env_int("GCG_TN_NOT_STACKED"))) {
+    int a = 0, b = 0, c = 0, d = 1, e = 0;
+    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) >= 3)
+      p.mg = a, p.ng = b, p.pd = c, p.wm = d, p.occ = e;
   }
   const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
   const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
@@ -1515,12 +1520,13 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   const dim3 grid(static_cast<unsigned>(n_tiles));
   const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
   const int remap = rmv ? std::atoi(rmv) : 1;
-#define GCG_TN_CASE(MG_, NG_, PD_, WM_)                                                      \
-  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_) {                            \
-    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_>), grid,                   \
+#define GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, OCC_)                                            \
+  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_ && p.occ == OCC_) {           \
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_, OCC_>), grid,             \
                        dim3(WM_ <= 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
                        B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);       \
   } else
+#define GCG_TN_CASE(MG_, NG_, PD_, WM_) GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, 0)
   GCG_TN_CASE(1, 2, 4, 1)
   GCG_TN_CASE(1, 2, 8, 1)
   GCG_TN_CASE(1, 1, 8, 1)
@@ -1535,8 +1541,14 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   GCG_TN_CASE(1, 3, 8, 0)
   GCG_TN_CASE(1, 3, 12, 0)
   GCG_TN_CASE(1, 3, 6, 0)
+  GCG_TN_CASE_OCC(1, 3, 2, 0, 2)
+  GCG_TN_CASE_OCC(1, 3, 3, 0, 2)
+  GCG_TN_CASE_OCC(1, 2, 8, 0, 2)
+  GCG_TN_CASE_OCC(1, 2, 4, 0, 2)
+  GCG_TN_CASE_OCC(1, 2, 6, 0, 2)
   { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
 #undef GCG_TN_CASE
+#undef GCG_TN_CASE_OCC
   GCG_HIP_CHECK(hipGetLastError());
   const int vec = (ldc % 4 == 0 && aligned(C, 16)) ? 1 : 0;
   const dim3 rgrid(static_cast<unsigned>(((N + 3) / 4 + 63) / 64),
