@@ -1074,31 +1074,37 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // 256*NG) padded N = 930 to 1024 columns -- 15 % of the MFMAs computed discarded columns.
   // World dW2 840k x 300 x 930: 960 padded columns, 105.8 -> 121.7 TFLOP/s; US dW2 270k x 300
   // x 256 (NG = 2): 87-103 -> 118 (tools/exp_tn_wave.py).
+  // NG = 3 runs at 2 waves per SIMD (PD = 3: 246 VGPRs, accumulators included) over ~8192 wave
+  // tiles: 129 vs 123 TFLOP/s at 1 wave per SIMD standalone, and inside the training step -- where
+  // the weight gradient shares the chip with the SpMM gathers on the main stream -- the shorter,
+  // CU-sharing waves overlap better: World step 44.4 -> 43.2 ms (tools/exp_tn_instep.py). NG = 2
+  // (US dW2, N = 256) measured best at 1 wave per SIMD, PD = 8, ~2048 tiles, in both settings.
   p.mg = 1, p.pd = 8;
+  int64_t slots = 2048;
   {
     const int64_t pad3 = (N + 191) / 192 * 192, pad2 = (N + 127) / 128 * 128;
     p.wm = 0, p.ng = pad3 <= pad2 ? 3 : 2;
+    if (p.ng == 3) p.pd = 3, p.occ = 2, slots = 8192;
   }
   // M <= 256 in whole 64-row bands and N <= 512 (the X-head gradient G^T.Xh: 1.4M x 300 x 256
   // as 300 x 256 with the roles below): M/64 waves stacked along M -- A (the narrow operand) is
   // then split over the waves and B read once per row: 85-89 -> 112-115 TFLOP/s. Not for the
   // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
   const bool stacked = M <= 256 && M % 64 == 0 && N <= 512;
-  if (stacked) p.ng = 1, p.wm = static_cast<int>(M / 64);
+  if (stacked) p.ng = 1, p.pd = 8, p.occ = 0, p.wm = static_cast<int>(M / 64), slots = 2048;
   // experiment knob: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes alone)
   if (const char* v = std::getenv("GCG_TN"); v && !(stacked && env_int("GCG_TN_NOT_STACKED"))) {
     int a = 0, b = 0, c = 0, d = 1, e = 0;
     if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) >= 3)
-      p.mg = a, p.ng = b, p.pd = c, p.wm = d, p.occ = e;
+      p.mg = a, p.ng = b, p.pd = c, p.wm = d, p.occ = e, slots = 2048;
   }
   const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
   const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
   p.mt = static_cast<int>((M + tm - 1) / tm);
   p.nt = static_cast<int>((N + tn - 1) / tn);
-  // ~2048 tiles: 2 workgroups per CU of the 256 CUs (WM = 0: the tiles are waves, 1 per SIMD,
-  // so 2 rounds of the 1024 SIMDs -- 1 round measured the same speed with 2x longer serial
-  // sums), at least 256 rows per split, 16-row aligned
-  int64_t slots = 2048;
+  // ~`slots` tiles per launch (2048: 2 workgroups per CU of the 256 CUs; per-wave tiles at 1
+  // wave per SIMD: 2 rounds of the 1024 SIMDs -- 1 round measured the same speed with 2x longer
+  // serial sums), at least 256 rows per split, 16-row aligned
   if (const char* v = std::getenv("GCG_TN_SLOTS")) slots = std::max(1, std::atoi(v));  // knob
   const int64_t want = std::max<int64_t>(1, slots / std::max(1, p.mt * p.nt));
   const int64_t max_s = std::max<int64_t>(1, R / 256);

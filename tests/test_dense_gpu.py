@@ -209,7 +209,8 @@ def test_gemm_tn_vs_float64(cuda, R, M, N):
     assert np.array_equal(C3, (C * np.float32(2.5)))
 
 
-@pytest.mark.parametrize("layout", ["1,2,8,1", "1,3,8,0", "1,2,8,0", "1,3,12,0", "1,1,8,4"])
+@pytest.mark.parametrize("layout", ["1,2,8,1", "1,3,8,0", "1,2,8,0", "1,3,12,0", "1,1,8,4",
+                                    "1,3,3,0,2", "1,2,6,0,2"])
 @pytest.mark.parametrize("R,M,N", [(4097, 300, 930), (70001, 256, 300), (513, 70, 129), (5, 3, 200)])
 def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, layout, monkeypatch):
     """Every split-K wave layout (GCG_TN=MG,NG,PD,WM: workgroup tiles WM = 1, per-wave tiles
