@@ -1092,8 +1092,12 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
   const bool stacked = M <= 256 && M % 64 == 0 && N <= 512;
   if (stacked) p.ng = 1, p.pd = 8, p.occ = 0, p.wm = static_cast<int>(M / 64), slots = 2048;
-  // experiment knob: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes alone)
-  if (const char* v = std::getenv("GCG_TN"); v && !(stacked && env_int("GCG_TN_NOT_STACKED"))) {
+  // experiment knobs: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes
+  // alone; GCG_TN_STACKED: a layout for the stacked shapes only)
+  const char* v = std::getenv("GCG_TN");
+  if (v && stacked && env_int("GCG_TN_NOT_STACKED")) v = nullptr;
+  if (const char* vs = std::getenv("GCG_TN_STACKED"); vs && stacked) v = vs;
+  if (v) {
     int a = 0, b = 0, c = 0, d = 1, e = 0;
     if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) >= 3)
       p.mg = a, p.ng = b, p.pd = c, p.wm = d, p.occ = e, slots = 2048;

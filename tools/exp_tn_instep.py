@@ -17,6 +17,8 @@ from graphconvgeo_amd.synth import CONFIGS, synthetic_features, synthetic_graph 
 
 variants = os.environ.get("TN_INSTEP", "default;1,2,8,1;1,3,2,0,2;1,3,3,0,2;1,2,8,0,2;1,2,6,0,2").split(";")
 orders = os.environ.get("TN_ORDERS", "propagate_first").split(",")
+# TN_KNOB=GCG_TN_STACKED: vary the X-head gradient's layout (the stacked shapes) instead of dW2's
+KNOB = os.environ.get("TN_KNOB", "GCG_TN")
 os.environ["GCG_TN_NOT_STACKED"] = "1"
 dev = torch.device("cuda:0")
 for name, order in [(c, o) for c in (sys.argv[1] if len(sys.argv) > 1 else
@@ -52,11 +54,11 @@ for name, order in [(c, o) for c in (sys.argv[1] if len(sys.argv) > 1 else
     res = {}
     for rnd in range(3):
         for v in variants:
-            os.environ.pop("GCG_TN", None)
+            os.environ.pop(KNOB, None)
             os.environ.pop("GCG_TN_SLOTS", None)
             if v != "default":
                 tile, _, slots = v.partition("@")
-                os.environ["GCG_TN"] = tile
+                os.environ[KNOB] = tile
                 if slots:
                     os.environ["GCG_TN_SLOTS"] = slots
             for _ in range(2):
@@ -67,7 +69,7 @@ for name, order in [(c, o) for c in (sys.argv[1] if len(sys.argv) > 1 else
                 step()
             torch.cuda.synchronize()
             res.setdefault(v, []).append(round((time.perf_counter() - t0) / 5 * 1e3, 3))
-    os.environ.pop("GCG_TN", None)
+    os.environ.pop(KNOB, None)
     os.environ.pop("GCG_TN_SLOTS", None)
     print(json.dumps({"config": name, "order": order, "main_prio": hi is not None,
                       "ms_per_step": res}), flush=True)
