@@ -437,7 +437,12 @@ def row_stride(k: int) -> int:
     304 (1216 B) every row starts 0 or 64 B into a line and spans exactly 10. Strides that are
     a multiple of 128 B (all rows on one alignment) are skipped: 1280-B rows measured slower
     than 1200-B ones (HBM channel interleave). Measured, World H.Z at K = 300: 6.84 -> 6.67-6.70
-    ms power-law, 9.37 -> 9.20-9.22 ms uniform (tools/gpu/ld_sweep.sh)."""
+    ms power-law, 9.37 -> 9.20-9.22 ms uniform (tools/gpu/ld_sweep.sh).
+    When no such stride exists within +32 floats (the first line's slack is too small: K = 500,
+    1500, the reference's default and tuned hidden sizes, tensormain.py:82,398), the next
+    multiple of 128 B puts every row on the minimal line count instead (round 3,
+    tools/exp_ld_k.py, World power-law / uniform): K = 500 at 512 floats 11.74 -> 10.99 /
+    16.14 -> 14.77 ms, K = 1500 at 1504 33.39 -> 31.89 / 44.18 -> 42.11 ms."""
     k4 = (k + 3) // 4 * 4
     if k < 32 or (4 * k) % 128 == 0:
         return k4
@@ -446,7 +451,7 @@ def row_stride(k: int) -> int:
         step = (4 * ld) % 128
         if step and 128 - math.gcd(step, 128) <= slack:  # row starts: multiples of gcd
             return ld
-    return k4
+    return (k + 31) // 32 * 32  # 128-B aligned rows: every row on the minimal line count
 
 
 def empty_dense(n: int, k: int, device, pad_to: int = 4) -> torch.Tensor:
