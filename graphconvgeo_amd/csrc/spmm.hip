@@ -215,6 +215,55 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
   }
 }
 
+// Narrow rows (round 3): K <= 256 / SUB floats, so a row needs only 64 / SUB lanes and a wave
+// accumulates SUB rows at once, one lane group per row (the whole-wave loop above would leave
+// 3/4 of the lanes idle at K = 64). Each group walks its own row [s, e) in storage order; the
+// (col, val) pairs are per-lane vector loads (one address per group), U gathers in flight, the
+// next batch's pairs loaded behind this batch's gathers. The wave runs to its longest row
+// (mlen, wave-uniform); a group past its row end loads row 0 / column 0 (valid addresses) and
+// keeps its sum by a select, so every row's additions are exactly the single-row sequence.
+template <int U>
+__device__ __forceinline__ void accumulate_sub(int s, int e, int mlen,
+                                               const int32_t* __restrict__ indices,
+                                               const float* __restrict__ vals,
+                                               const float* __restrict__ Z, int64_t ldz, int gcol,
+                                               Vec<4>& acc) {
+  int cn[U];
+  float vn[U];
+  auto load_idx = [&](int j0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int idx = s + j0 + u;
+      const int ix = idx < e ? idx : 0;
+      cn[u] = indices[ix];
+      vn[u] = vals[ix];
+    }
+  };
+  if (mlen > 0) load_idx(0);
+  for (int j = 0; j < mlen; j += U) {
+    int c[U];
+    float v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      c[u] = cn[u];
+      v[u] = vn[u];
+    }
+    Vec<4> z[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) z[u] = load_vec<4>(Z + static_cast<int64_t>(c[u]) * ldz + gcol);
+    if (j + U < mlen) load_idx(j + U);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool ok = s + j + u < e;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float t = acc.x[q] + v[u] * z[u].x[q];
+        acc.x[q] = ok ? t : acc.x[q];
+      }
+    }
+  }
+}
+
 // Barrier for LDS hand-over between the waves of a workgroup: retires this wave's LDS
 // operations only (the gathers stay in flight across it), then s_barrier.
 __device__ __forceinline__ void lds_handover_barrier() {
@@ -371,9 +420,10 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
 // The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
 // (coop_row); the other tasks one wave each, in the blocks after them.
-template <int VEC, int NCH, int U, int WPB = kWavesPerBlock>
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1>
 __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
-    const int4* __restrict__ tasks, int n_tasks, int n_coop, const int32_t* __restrict__ indptr,
+    const int4* __restrict__ tasks, int n_tasks, int n_coop, int n_out,
+    const int32_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
@@ -412,8 +462,8 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
   if (tasks != nullptr) {
     t = tasks[w];
     t.x = uniform(t.x); t.y = uniform(t.y); t.z = uniform(t.z); t.w = uniform(t.w);
-  } else {
-    t = make_int4(w, w + 1, -1, -1);
+  } else {  // plan-less: SUB consecutive rows per wave
+    t = make_int4(w * SUB, min(w * SUB + SUB, n_out), -1, -1);
   }
 
   Vec<VEC> acc[NCH];
@@ -427,6 +477,49 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
       if (on[k]) store_vec<VEC>(dst + col[k], acc[k]);
+    return;
+  }
+
+  if constexpr (SUB > 1) {
+    static_assert(VEC == 4 && NCH == 1, "narrow rows: one dwordx4 per lane");
+    constexpr int LG = kWave / SUB;  // lanes per row
+    const int g = lane / LG;
+    const int scol = (lane % LG) * 4;  // one panel: K <= 4 * LG
+    const bool son = scol < K;
+    const int sgcol = son ? scol : 0;
+    Vec<4> sbv;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) sbv.x[q] = 0.0f;
+    if (bias != nullptr) sbv = load_vec<4>(bias + sgcol);
+    for (int pb = t.x; pb < t.y; pb += SUB) {
+      const int p = pb + g;
+      const bool live = p < t.y;
+      const int pp = live ? p : t.x;
+      const int r = out_rows ? out_rows[pp] : pp;
+      const int rs = indptr[r];
+      const int re = live ? indptr[r + 1] : rs;
+      int mlen = re - rs;  // the longest of the wave's SUB rows (every group's first lane)
+#pragma unroll
+      for (int o = LG; o < kWave; o <<= 1) mlen = max(mlen, __shfl_xor(mlen, o, kWave));
+      mlen = uniform(mlen);
+      Vec<4> acc;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc.x[q] = 0.0f;
+      accumulate_sub<U>(rs, re, mlen, indices, vals, Z, ldz, sgcol, acc);
+      if (!(live && son)) continue;
+      if (bias != nullptr) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc.x[q] = acc.x[q] + sbv.x[q];
+      }
+      if (gate != nullptr) store_gate<4>(gate + static_cast<int64_t>(p) * ldgate + scol, acc);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) acc.x[q] = apply_act(acc.x[q], act);
+      float* yrow = Y + static_cast<int64_t>(p) * ldy + scol;
+      if (nt_store)
+        store_vec_nt<4>(yrow, acc);
+      else
+        store_vec<4>(yrow, acc);
+    }
     return;
   }
 
@@ -520,14 +613,17 @@ struct LaunchArgs {
   int n_coop = 0;  // leading tasks run by a whole workgroup each (ordered long rows)
 };
 
-template <int VEC, int NCH, int U, int WPB>
+template <int VEC, int NCH, int U, int WPB, int SUB = 1>
 void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
-  const dim3 grid(a.n_coop + (a.n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
+  // plan-less: one wave per SUB consecutive rows
+  const int n_tasks = a.tasks == nullptr ? (a.n_tasks + SUB - 1) / SUB : a.n_tasks;
+  const dim3 grid(a.n_coop + (n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
   static const int xcd = env_int("GCG_XCD_REMAP");
   const int nts = env_int("GCG_SPMM_NT_STORE");
-  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB>), grid, dim3(kWave * WPB), 0, stream,
-                     a.tasks, a.n_tasks, a.n_coop, a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K,
-                     a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate, a.ldgate, nts);
+  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB>), grid, dim3(kWave * WPB), 0, stream,
+                     a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows,
+                     a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate,
+                     a.ldgate, nts);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
@@ -546,6 +642,19 @@ void launch_rows_f(const LaunchArgs& a, int n_panels, hipStream_t stream) {
 
 template <int VEC, int NCH>
 void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
+  if constexpr (VEC == 4 && NCH == 1) {
+    // Narrow rows, plan-less (rowwise) only: 4 rows per wave at K <= 64, 2 at K <= 96. The wave
+    // runs to its longest row, so this pays where rows are alike -- 'auto' takes rowwise only
+    // on hub-free graphs -- and loses on a planned power-law task (ordered, World: K = 96 2.08
+    // -> 2.54 ms) and at K = 128 (3.09 -> 3.20); World uniform: K = 16 / 32 / 64 1.93 / 1.94 /
+    // 2.19 -> 0.91 / 0.93 / 1.48 ms, K = 96 2.50 -> 2.39 (tools/exp_spmm_narrow.py).
+    // GCG_SPMM_SUB = 1 / 2 / 4 forces the rows per wave (experiments, tests).
+    const int sub_env = env_int("GCG_SPMM_SUB");
+    const int sub = sub_env ? sub_env
+                            : (a.tasks != nullptr ? 1 : a.K <= 64 ? 4 : a.K <= 96 ? 2 : 1);
+    if (sub == 4 && a.K <= 64) return launch_rows_u<4, 1, 16, kWavesPerBlock, 4>(a, n_panels, stream);
+    if (sub >= 2 && a.K <= 128) return launch_rows_u<4, 1, 16, kWavesPerBlock, 2>(a, n_panels, stream);
+  }
   if constexpr (VEC == 4 && NCH == 2) {
     static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
     if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);

@@ -112,6 +112,44 @@ def test_bias_relu_and_rows_subset(cuda, mode):
     assert np.array_equal(Y2, ref)
 
 
+@pytest.mark.parametrize("K", [4, 16, 60, 64, 68, 96, 124, 128])
+@pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
+def test_narrow_rows_subwave_path(cuda, K, mode, monkeypatch):
+    """Narrow rows, 2 (K <= 128) or 4 (K <= 64) per wave, one lane group per row
+    (spmm_rows_kernel<4, 1, 16, 4, SUB>; the default takes it plan-less at K <= 96, forced here
+    in every mode): bitwise equal to the whole-wave path (GCG_SPMM_SUB=1) and to the oracle in
+    the bitwise modes, with bias + rectify + gate bytes, a row subset with duplicates, empty rows,
+    a cooperative hub row (ordered) and split rows (fast)."""
+    H = rand_csr(777, 600, 10, seed=11 + K, long_rows=[(9, 4100), (500, 700)], empty_frac=0.15)
+    Z = np.random.default_rng(K).standard_normal((600, K)).astype(np.float32)
+    b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
+    rows = np.random.default_rng(5).integers(0, 777, size=401).astype(np.int32)
+    rows[:3] = 9
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    Zd, bd = to_dev(Z, cuda), to_dev(b, cuda)
+    outs = {}
+    for sub in ("4" if K <= 64 else "2", "1"):  # forced, so the planned modes take it too
+        monkeypatch.setenv("GCG_SPMM_SUB", sub)
+        gate = gs.empty_gate(H.shape[0], K, cuda)
+        Y = gs.spmm(A, Zd, bias=bd, act="relu", mode=mode, gate=gate, task_nnz=256)
+        Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
+        outs[sub] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
+    for a, c in zip(outs["4" if K <= 64 else "2"], outs["1"]):
+        assert np.array_equal(a, c)
+    Y, gate, Ys = outs["1"]
+    ref = O.spmm_f32(H, Z, bias=b, act="relu")
+    pre = O.spmm_f32(H, Z, bias=b)
+    refs = O.spmm_f32(H, Z, rows=rows)
+    if mode == "fast":
+        assert np.abs(Y - ref).max() <= 1e-5
+        unsplit = np.diff(H.indptr) <= 256
+        assert np.array_equal(Y[unsplit], ref[unsplit])
+    else:
+        assert np.array_equal(Y, ref) and np.array_equal(Ys, refs)
+        want = np.where(pre > 0, 2, np.where(pre == 0, 1, 0)).astype(np.uint8)
+        assert np.array_equal(gate, want)
+
+
 def test_unsorted_and_duplicate_entries(cuda):
     H = rand_csr(300, 300, 15, seed=9, sort=False, dups=True)
     assert not H.has_canonical_format
