@@ -70,6 +70,21 @@ __device__ __forceinline__ Vec<VEC> load_vec(const float* __restrict__ p) {
   return r;
 }
 
+// Non-temporal load (experiment: cold gathered rows, GCG_SPMM_HC).
+template <int VEC>
+__device__ __forceinline__ Vec<VEC> load_vec_nt(const float* __restrict__ p) {
+  Vec<VEC> r;
+  if constexpr (VEC == 4) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const f4v t = __builtin_nontemporal_load(reinterpret_cast<const f4v*>(p));
+    r.x[0] = t[0]; r.x[1] = t[1]; r.x[2] = t[2]; r.x[3] = t[3];
+  } else {
+#pragma unroll
+    for (int q = 0; q < VEC; ++q) r.x[q] = __builtin_nontemporal_load(p + q);
+  }
+  return r;
+}
+
 // Non-temporal (streaming) store: Y is written once and not re-read by this kernel, so it
 // need not displace the gathered operand's hot rows from the caches (experiment knob
 // GCG_SPMM_NT_STORE=1).
@@ -123,7 +138,7 @@ __device__ __forceinline__ void store_gate(uint8_t* __restrict__ p, const Vec<VE
 }
 
 // Accumulate nonzeros [s, e) of one row into acc, storage order, U gathers in flight.
-template <int VEC, int NCH, int U>
+template <int VEC, int NCH, int U, int HC = 0>
 __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __restrict__ indices,
                                                  const float* __restrict__ vals,
                                                  const float* __restrict__ Z, int64_t ldz,
@@ -164,10 +179,21 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
     Vec<VEC> z[U][NCH];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+      if constexpr (HC) {  // experiment: sign bit = cold column -> non-temporal gather
+        const float* zrow = Z + static_cast<int64_t>(c[u] & 0x7fffffff) * ldz;
+        if (c[u] < 0) {
 #pragma unroll
-      for (int k = 0; k < NCH; ++k)
-        z[u][k] = load_vec<VEC>(zrow + col[k]);
+          for (int k = 0; k < NCH; ++k) z[u][k] = load_vec_nt<VEC>(zrow + col[k]);
+        } else {
+#pragma unroll
+          for (int k = 0; k < NCH; ++k) z[u][k] = load_vec<VEC>(zrow + col[k]);
+        }
+      } else {
+        const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+#pragma unroll
+        for (int k = 0; k < NCH; ++k)
+          z[u][k] = load_vec<VEC>(zrow + col[k]);
+      }
     }
 #if GCG_SPMM_IDX_PREFETCH
     {
@@ -200,7 +226,7 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
 #pragma unroll
     for (int u = 0; u < U - 1; ++u)
       if (u < rem) {
-        const float* zrow = Z + static_cast<int64_t>(c[u]) * ldz;
+        const float* zrow = Z + static_cast<int64_t>(HC ? (c[u] & 0x7fffffff) : c[u]) * ldz;
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
           z[u][k] = load_vec<VEC>(zrow + col[k]);
@@ -281,7 +307,7 @@ __device__ __forceinline__ void lds_handover_barrier() {
 // the one the single-wave loop makes, in the same order: bitwise equal (scipy csr_matvecs).
 // A wave issues its next batch's gathers right after its own hand-over, so they fly while the
 // later waves of this batch add. LDS: one row sum (<= 512 floats).
-template <int VEC, int NCH, int U, int WPB>
+template <int VEC, int NCH, int U, int WPB, int HC = 0>
 __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
                                          const int32_t* __restrict__ indices,
                                          const float* __restrict__ vals,
@@ -323,6 +349,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c[u] = __builtin_amdgcn_readlane(ci, u);
+      if constexpr (HC) c[u] &= 0x7fffffff;  // experiment: strip the cold-column bit
       v[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vi), u));
     }
 #pragma unroll
@@ -420,7 +447,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
 // The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
 // (coop_row); the other tasks one wave each, in the blocks after them.
-template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1>
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0>
 __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int4* __restrict__ tasks, int n_tasks, int n_coop, int n_out,
     const int32_t* __restrict__ indptr,
@@ -451,7 +478,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
   }
   if (blk < n_coop) {  // a whole-workgroup long row (uniform across the block)
     __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
-    coop_row<VEC, NCH, U, WPB>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z, ldz,
+    coop_row<VEC, NCH, U, WPB, HC>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z, ldz,
                                col, gcol, on, Y, ldy, bias, act, gate, ldgate, sacc);
     return;
   }
@@ -472,7 +499,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     for (int k = 0; k < NCH; ++k)
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = 0.0f;
-    accumulate_range<VEC, NCH, U>(t.y, t.z, indices, vals, Z, ldz, gcol, acc);
+    accumulate_range<VEC, NCH, U, HC>(t.y, t.z, indices, vals, Z, ldz, gcol, acc);
     float* dst = ws + static_cast<int64_t>(t.w) * ldws;
 #pragma unroll
     for (int k = 0; k < NCH; ++k)
@@ -545,7 +572,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     for (int k = 0; k < NCH; ++k)
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = 0.0f;
-    accumulate_range<VEC, NCH, U>(s, e, indices, vals, Z, ldz, gcol, acc);
+    accumulate_range<VEC, NCH, U, HC>(s, e, indices, vals, Z, ldz, gcol, acc);
     float* yrow = Y + static_cast<int64_t>(p) * ldy;
 #pragma unroll
     for (int k = 0; k < NCH; ++k) {
@@ -613,14 +640,14 @@ struct LaunchArgs {
   int n_coop = 0;  // leading tasks run by a whole workgroup each (ordered long rows)
 };
 
-template <int VEC, int NCH, int U, int WPB, int SUB = 1>
+template <int VEC, int NCH, int U, int WPB, int SUB = 1, int HC = 0>
 void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   // plan-less: one wave per SUB consecutive rows
   const int n_tasks = a.tasks == nullptr ? (a.n_tasks + SUB - 1) / SUB : a.n_tasks;
   const dim3 grid(a.n_coop + (n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
   static const int xcd = env_int("GCG_XCD_REMAP");
   const int nts = env_int("GCG_SPMM_NT_STORE");
-  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB>), grid, dim3(kWave * WPB), 0, stream,
+  hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows,
                      a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate,
                      a.ldgate, nts);
@@ -662,6 +689,8 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     // planned tasks of >= 256 nnz: U = 16 since the (col, val) stream is software-pipelined
     // (late round 2): 163 VGPRs / 3 waves per SIMD and fewer SGPR spills than U = 24 (222 VGPRs,
     // 2 waves): World power-law 6.60 vs 6.71 ms (three alternating runs each, one box)
+    // experiment: GCG_SPMM_HC=1 -- indices carry a cold-column sign bit (tools/exp_hot_cold.py)
+    if (env_int("GCG_SPMM_HC")) return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 1>(a, n_panels, stream);
     if (inflight != 64 && a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
     // plan-less, one row per wave, on a large graph (sparse.resolve_auto picks it for graphs
     // without hub rows): U = 16, 3 waves/SIMD -- Twitter-World uniform 9.35-9.36 vs 9.41-9.44 ms
