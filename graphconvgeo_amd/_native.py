@@ -45,6 +45,8 @@ SIGNATURES = {
                                         _p, C.c_int, _p, _i64, _p, _i64, _p]),
     "gcg_spmm_csr_f32_planned_gate": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
                                                 C.c_int, _p, _i64, _p, C.c_size_t, _p]),
+    "gcg_spmm_csr_f32_planned_hint": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
+                                                C.c_int, _p, _i64, _p, C.c_size_t, _p, _p]),
     "gcg_relu_backward_gate_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, _i64, _p, _i64, _p, _p,
                                              C.c_size_t, _p]),
     "gcg_spmm_plan_host": (C.c_int, [_i64, _p, _p, _i64, _i64, C.c_int, _p, _i64, _pi64, _p,

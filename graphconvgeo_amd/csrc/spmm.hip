@@ -638,6 +638,9 @@ struct LaunchArgs {
   uint8_t* gate = nullptr;  // rectify gate bytes (nullable), row stride ldgate
   int64_t ldgate = 0;
   int n_coop = 0;  // leading tasks run by a whole workgroup each (ordered long rows)
+  // gather hint: the column indices with a cold-column sign bit (nullable); used by the
+  // dwordx4 x 2 launch only, every other launch reads `indices`
+  const int32_t* hint = nullptr;
 };
 
 template <int VEC, int NCH, int U, int WPB, int SUB = 1, int HC = 0>
@@ -689,8 +692,12 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     // planned tasks of >= 256 nnz: U = 16 since the (col, val) stream is software-pipelined
     // (late round 2): 163 VGPRs / 3 waves per SIMD and fewer SGPR spills than U = 24 (222 VGPRs,
     // 2 waves): World power-law 6.60 vs 6.71 ms (three alternating runs each, one box)
-    // experiment: GCG_SPMM_HC=1 -- indices carry a cold-column sign bit (tools/exp_hot_cold.py)
-    if (env_int("GCG_SPMM_HC")) return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 1>(a, n_panels, stream);
+    // gather hint: cold columns' rows gathered non-temporally (gcg_spmm_csr_f32_planned_hint)
+    if (a.hint != nullptr && !env_int("GCG_SPMM_NO_HINT")) {
+      LaunchArgs h = a;
+      h.indices = a.hint;
+      return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 1>(h, n_panels, stream);
+    }
     if (inflight != 64 && a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
     // plan-less, one row per wave, on a large graph (sparse.resolve_auto picks it for graphs
     // without hub rows): U = 16, 3 waves/SIMD -- Twitter-World uniform 9.35-9.36 vs 9.41-9.44 ms
@@ -1063,6 +1070,17 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
                                          int64_t ldy, const float* bias, int act, uint8_t* gate,
                                          int64_t ldgate, void* workspace,
                                          size_t workspace_bytes, gcg_stream_t stream) {
+  return gcg_spmm_csr_f32_planned_hint(plan, indptr, indices, vals, Z, ldz, K, Y, ldy, bias, act,
+                                       gate, ldgate, workspace, workspace_bytes, nullptr, stream);
+}
+
+gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                         const int32_t* indices, const float* vals,
+                                         const float* Z, int64_t ldz, int64_t K, float* Y,
+                                         int64_t ldy, const float* bias, int act, uint8_t* gate,
+                                         int64_t ldgate, void* workspace,
+                                         size_t workspace_bytes, const int32_t* gather_hint,
+                                         gcg_stream_t stream) {
   if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
   if (gcg_status st = check_dense(Z, ldz, Y, ldy, K, bias, act)) return st;
   if (gcg_status st = check_gate(gate, ldgate, K, act)) return st;
@@ -1078,7 +1096,8 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
   float* ws = need > 0 ? static_cast<float*>(workspace) : nullptr;
   hipStream_t st = static_cast<hipStream_t>(stream);
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
-               Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate, plan->n_coop};
+               Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate, plan->n_coop,
+               gather_hint};
   if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
   if (plan->n_long > 0) {
     const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);

@@ -139,6 +139,23 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
                                          size_t workspace_bytes, gcg_stream_t stream);
 
 /*
+ * Planned SpMM with a gather hint (round 3): gather_hint (device, nullable, nnz int32) is the
+ * column index array with bit 31 set on every "cold" column -- a column whose Z row the caller
+ * expects to be gathered rarely. Cold rows are gathered with non-temporal loads, so they do not
+ * displace the hot rows (hub nodes of a power-law graph) from the L2 / Infinity Cache; the
+ * result is bitwise the one without the hint (only the cache policy of the loads changes).
+ * Used by the dwordx4 launch of widths 257..512 per column panel (K = 300, 1500); every other
+ * launch reads `indices`. graphconvgeo_amd.sparse builds the hint (DeviceCSR.gather_hint).
+ */
+gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_t* indptr,
+                                         const int32_t* indices, const float* vals,
+                                         const float* Z, int64_t ldz, int64_t K, float* Y,
+                                         int64_t ldy, const float* bias, int act, uint8_t* gate,
+                                         int64_t ldgate, void* workspace,
+                                         size_t workspace_bytes, const int32_t* gather_hint,
+                                         gcg_stream_t stream);
+
+/*
  * Host-only planner (no device memory, no HIP calls): the task list the plan uses,
  * exposed for testing and for host-side tools. `tasks_host` receives n_tasks int32
  * quadruples {a, b, c, d}: d < 0 -> rows of positions [a, b); d >= 0 -> segment of

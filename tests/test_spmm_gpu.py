@@ -150,6 +150,53 @@ def test_narrow_rows_subwave_path(cuda, K, mode, monkeypatch):
         assert np.array_equal(gate, want)
 
 
+@pytest.mark.parametrize("mode", ["ordered", "fast"])
+@pytest.mark.parametrize("K", [300, 512, 1500])
+def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
+    """The gather hint (cold columns' rows gathered non-temporally, DeviceCSR.gather_hint ->
+    gcg_spmm_csr_f32_planned_hint) changes the loads' cache policy only: bitwise the hint-less
+    result and the oracle, with cooperative hub rows (ordered), split rows (fast), a row
+    subset, bias + rectify + gate. Thresholds lowered so a test-sized graph takes the hint."""
+    monkeypatch.setattr(gs, "GATHER_HINT_MIN_TABLE", 0)
+    monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 1 << 20)
+    H = synthetic_graph(20_000, 200_000)  # power-law: hub columns
+    Z = dense(20_000, K)
+    b = np.random.default_rng(K).standard_normal(K).astype(np.float32)
+    rows = np.random.default_rng(3).integers(0, 20_000, size=5000).astype(np.int32)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    hint = A.gather_hint(4 * min(gs.row_stride(K), 512))
+    assert hint is not None and int((hint < 0).sum()) > 0
+    assert torch.equal(hint & 0x7FFFFFFF, A.indices)
+    Zd = gs.empty_dense(20_000, K, cuda).copy_(to_dev(Z, cuda))
+    outs = {}
+    for off in ("0", "1"):
+        monkeypatch.setenv("GCG_SPMM_NO_HINT", off)
+        gate = gs.empty_gate(20_000, K, cuda)
+        Y = gs.spmm(A, Zd, bias=to_dev(b, cuda), act="relu", mode=mode, gate=gate, task_nnz=256)
+        Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
+        outs[off] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
+    for a, c in zip(outs["0"], outs["1"]):
+        assert np.array_equal(a, c)
+    if mode == "ordered":
+        assert np.array_equal(outs["0"][0], O.spmm_f32(H, Z, bias=b, act="relu"))
+        assert np.array_equal(outs["0"][2], O.spmm_f32(H, Z, rows=rows))
+
+
+def test_gather_hint_off_where_it_does_not_pay(cuda):
+    """No hint on a small operand (the Infinity Cache holds it) or a graph without hub columns."""
+    A = gs.DeviceCSR.from_scipy(synthetic_graph(20_000, 200_000), cuda, symmetric=True)
+    assert A.gather_hint(1216) is None  # 24 MB operand < GATHER_HINT_MIN_TABLE
+    U = gs.DeviceCSR.from_scipy(synthetic_graph(20_000, 200_000, kind="uniform"), cuda,
+                                symmetric=True)
+    old = gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES
+    try:
+        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES = 0, 1 << 20
+        assert U.gather_hint(1216) is None  # the top 862 columns hold < 25 % of the nonzeros
+        assert A.gather_hint(1216) is not None  # ... the power-law graph's do
+    finally:
+        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES = old
+
+
 def test_unsorted_and_duplicate_entries(cuda):
     H = rand_csr(300, 300, 15, seed=9, sort=False, dups=True)
     assert not H.has_canonical_format

@@ -1,15 +1,13 @@
 #!/usr/bin/env python
-"""Experiment: keep the hub rows of Z in the L2 by gathering every other row with a
-non-temporal load (GCG_SPMM_HC=1: the kernel reads a cold-column sign bit from the indices).
-On the power-law World graph ~40 % of the gathers hit the top ~2,000 rows (2.4 MB, inside one
-XCD's 4 MB L2), yet L2->fabric bytes are 0.95x the edge-centric count. Hot set = the N most
-frequent columns; N = 0 (all cold) and N = n (all hot: the branch alone) bracket it.
-HIP events, interleaved rounds, outputs compared bitwise with the default kernel."""
+"""Gather hint (DeviceCSR.gather_hint, gcg_spmm_csr_f32_planned_hint): the rows of all but the
+most frequent columns of H are gathered with non-temporal loads so the hub rows stay in the
+L2 / Infinity Cache. Hot-set sizes (sparse.GATHER_HINT_HOT_BYTES) against no hint
+(GCG_SPMM_NO_HINT=1), H.Z at K = 300 on the Twitter-World and Twitter-US graphs, the mode auto
+resolves to, interleaved rounds, outputs compared bitwise. HIP events, mean of 10."""
 import json
 import os
 import sys
 
-import numpy as np
 import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -17,28 +15,20 @@ from graphconvgeo_amd import sparse as gs  # noqa: E402
 from graphconvgeo_amd.synth import CONFIGS, synthetic_graph  # noqa: E402
 
 dev = torch.device("cuda:0")
-cfg = CONFIGS["twitter-world"]
-K = 300
-for kind in (sys.argv[1] if len(sys.argv) > 1 else "powerlaw").split(","):
+K = int(os.environ.get("HINT_K", "300"))
+sizes_mb = [int(x) for x in os.environ.get("HINT_MB", "8,16,32,64").split(",")]
+for spec in (sys.argv[1] if len(sys.argv) > 1 else "twitter-world:powerlaw,twitter-us:powerlaw,"
+             "twitter-world:uniform").split(","):
+    name, kind = spec.split(":")
+    cfg = CONFIGS[name]
     H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
     n, nnz = H.shape[0], H.nnz
     A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
     mode = gs.resolve_auto(A)
     Z = gs.empty_dense(n, K, dev).copy_(torch.randn((n, K), device=dev))
     Y = gs.empty_dense(n, K, dev)
+    os.environ["GCG_SPMM_NO_HINT"] = "1"
     ref = gs.spmm(A, Z, mode=mode).clone()
-    orig = A.indices.clone()
-    counts = np.bincount(H.indices, minlength=n)
-    order = np.argsort(-counts, kind="stable")
-    variants = {}
-    for nh in (0, 1000, 2000, 3000, 6000, 12000, n):
-        hot = np.zeros(n, dtype=bool)
-        hot[order[:nh]] = True
-        share = float(counts[hot].sum() / nnz)
-        cold_bit = torch.as_tensor(~hot, device=dev)[orig.long()]
-        flagged = torch.where(cold_bit, orig | torch.tensor(-2**31, dtype=torch.int32, device=dev), orig)
-        variants[nh] = (flagged, share)
-    B = 4 * (n + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n
 
     def timed():
         for _ in range(3):
@@ -50,21 +40,20 @@ for kind in (sys.argv[1] if len(sys.argv) > 1 else "powerlaw").split(","):
         e.record()
         torch.cuda.synchronize()
         return round(s.elapsed_time(e) / 10, 3)
-    res = {}
+    res, used = {}, {}
     for rnd in range(3):
-        os.environ.pop("GCG_SPMM_HC", None)
-        A.indices.copy_(orig)
-        res.setdefault("default", []).append(timed())
-        for nh, (flagged, share) in variants.items():
-            A.indices.copy_(flagged)
-            os.environ["GCG_SPMM_HC"] = "1"
-            t = timed()
-            ok = bool(torch.equal(Y, ref))
-            os.environ.pop("GCG_SPMM_HC", None)
-            res.setdefault(f"hot={nh} ({share:.2f} of nnz)", []).append(t)
-            assert ok, f"hot={nh}: result differs"
-    A.indices.copy_(orig)
-    print(json.dumps({"graph": kind, "mode": mode, "ms": res,
-                      "GBps_default": round(B / min(res["default"]) / 1e6, 1)}), flush=True)
+        os.environ["GCG_SPMM_NO_HINT"] = "1"
+        res.setdefault("no hint", []).append(timed())
+        os.environ.pop("GCG_SPMM_NO_HINT", None)
+        for mb in sizes_mb:
+            gs.GATHER_HINT_HOT_BYTES = mb << 20
+            used[mb] = A.gather_hint(4 * min(Z.stride(0), 512)) is not None
+            res.setdefault(f"hot {mb} MB", []).append(timed())
+            assert torch.equal(Y, ref), f"hint {mb} MB changed the result"
+    gs.GATHER_HINT_HOT_BYTES = 32 << 20
+    B = 4 * (n + 1) + 8 * nnz + 4 * K * nnz + 4 * K * n
+    print(json.dumps({"graph": spec, "mode": mode, "K": K, "ms": res, "hint_used": used,
+                      "GBps_no_hint": round(B / min(res["no hint"]) / 1e6, 1),
+                      "GBps_32MB": round(B / min(res.get("hot 32 MB", [1e9])) / 1e6, 1)}), flush=True)
     del A, Z, Y, ref
     torch.cuda.empty_cache()
