@@ -157,6 +157,7 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
     gcg_spmm_csr_f32_planned_hint) changes the loads' cache policy only: bitwise the hint-less
     result and the oracle, with cooperative hub rows (ordered), split rows (fast), a row
     subset, bias + rectify + gate. Thresholds lowered so a test-sized graph takes the hint."""
+    monkeypatch.setattr(gs, "GATHER_HINT", True)
     monkeypatch.setattr(gs, "GATHER_HINT_MIN_TABLE", 0)
     monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 1 << 20)
     H = synthetic_graph(20_000, 200_000)  # power-law: hub columns
@@ -182,19 +183,20 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
         assert np.array_equal(outs["0"][2], O.spmm_f32(H, Z, rows=rows))
 
 
-def test_gather_hint_off_where_it_does_not_pay(cuda):
+def test_gather_hint_off_where_it_does_not_pay(cuda, monkeypatch):
     """No hint on a small operand (the Infinity Cache holds it) or a graph without hub columns."""
+    monkeypatch.setattr(gs, "GATHER_HINT", True)
     A = gs.DeviceCSR.from_scipy(synthetic_graph(20_000, 200_000), cuda, symmetric=True)
     assert A.gather_hint(1216) is None  # 24 MB operand < GATHER_HINT_MIN_TABLE
     U = gs.DeviceCSR.from_scipy(synthetic_graph(20_000, 200_000, kind="uniform"), cuda,
                                 symmetric=True)
-    old = gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES
+    old = gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES, gs.GATHER_HINT
     try:
-        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES = 0, 1 << 20
+        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES, gs.GATHER_HINT = 0, 1 << 20, True
         assert U.gather_hint(1216) is None  # the top 862 columns hold < 25 % of the nonzeros
         assert A.gather_hint(1216) is not None  # ... the power-law graph's do
     finally:
-        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES = old
+        gs.GATHER_HINT_MIN_TABLE, gs.GATHER_HINT_HOT_BYTES, gs.GATHER_HINT = old
 
 
 def test_unsorted_and_duplicate_entries(cuda):

@@ -15,6 +15,7 @@ from graphconvgeo_amd import sparse as gs  # noqa: E402
 from graphconvgeo_amd.synth import CONFIGS, synthetic_graph  # noqa: E402
 
 dev = torch.device("cuda:0")
+gs.GATHER_HINT = True
 K = int(os.environ.get("HINT_K", "300"))
 sizes_mb = [int(x) for x in os.environ.get("HINT_MB", "8,16,32,64").split(",")]
 for spec in (sys.argv[1] if len(sys.argv) > 1 else "twitter-world:powerlaw,twitter-us:powerlaw,"
