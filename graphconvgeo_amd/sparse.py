@@ -75,7 +75,7 @@ TMATMUL_HEAD_SIDE_STREAM = True
 # the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes. Measured on the World
 # power-law graph, K = 300 (tools/exp_hot_cold.py, interleaved): hot sets of 12k / 25k / 50k rows
 # (15 / 30 / 61 MB) 6.40 / 6.34 / 6.49 ms vs 6.80 without; every row non-temporal 7.71 vs 6.54.
-GATHER_HINT = False  # on after its GPU validation (see DESIGN)
+GATHER_HINT = True
 GATHER_HINT_HOT_BYTES = 32 << 20
 GATHER_HINT_MIN_SHARE = 0.25
 GATHER_HINT_MIN_TABLE = 512 << 20

@@ -159,7 +159,7 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
     subset, bias + rectify + gate. Thresholds lowered so a test-sized graph takes the hint."""
     monkeypatch.setattr(gs, "GATHER_HINT", True)
     monkeypatch.setattr(gs, "GATHER_HINT_MIN_TABLE", 0)
-    monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 1 << 20)
+    monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 4 << 20)  # 2k-3.4k hot rows: 48-59 % of nnz
     H = synthetic_graph(20_000, 200_000)  # power-law: hub columns
     Z = dense(20_000, K)
     b = np.random.default_rng(K).standard_normal(K).astype(np.float32)
