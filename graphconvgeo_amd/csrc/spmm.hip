@@ -639,7 +639,7 @@ struct LaunchArgs {
   int64_t ldgate = 0;
   int n_coop = 0;  // leading tasks run by a whole workgroup each (ordered long rows)
   // gather hint: the column indices with a cold-column sign bit (nullable); used by the
-  // dwordx4 x 2 launch only, every other launch reads `indices`
+  // dwordx4 launches (NCH 1 and 2), every other launch reads `indices`
   const int32_t* hint = nullptr;
 };
 
@@ -679,6 +679,11 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     // -> 2.54 ms) and at K = 128 (3.09 -> 3.20); World uniform: K = 16 / 32 / 64 1.93 / 1.94 /
     // 2.19 -> 0.91 / 0.93 / 1.48 ms, K = 96 2.50 -> 2.39 (tools/exp_spmm_narrow.py).
     // GCG_SPMM_SUB = 1 / 2 / 4 forces the rows per wave (experiments, tests).
+    if (a.hint != nullptr && !env_int("GCG_SPMM_NO_HINT")) {  // gather hint (planned only)
+      LaunchArgs h = a;
+      h.indices = a.hint;
+      return launch_rows_u<4, 1, 16, kWavesPerBlock, 1, 1>(h, n_panels, stream);
+    }
     const int sub_env = env_int("GCG_SPMM_SUB");
     const int sub = sub_env ? sub_env
                             : (a.tasks != nullptr ? 1 : a.K <= 64 ? 4 : a.K <= 96 ? 2 : 1);

@@ -74,7 +74,8 @@ TMATMUL_HEAD_SIDE_STREAM = True
 # whose gathered rows fit GATHER_HINT_HOT_BYTES; used when they carry >= GATHER_HINT_MIN_SHARE of
 # the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes. Measured on the World
 # power-law graph, K = 300 (tools/exp_hot_cold.py, interleaved): hot sets of 12k / 25k / 50k rows
-# (15 / 30 / 61 MB) 6.40 / 6.34 / 6.49 ms vs 6.80 without; every row non-temporal 7.71 vs 6.54.
+# (15 / 30 / 61 MB) 6.40 / 6.34 / 6.49 ms vs 6.80 without; every row non-temporal 7.71 vs 6.54;
+# K = 256: 4.96 (16 MB) / 5.10 (32 MB) vs 5.36 ms, K = 128: 2.36 vs 2.43 ms.
 GATHER_HINT = True
 GATHER_HINT_HOT_BYTES = 32 << 20
 GATHER_HINT_MIN_SHARE = 0.25
@@ -593,7 +594,7 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         else:
             plan = A.plan(sel, ordered=(mode == "ordered"), task_nnz=task_nnz)
             ws = plan.workspace(K)
-            hint = A.gather_hint(4 * min(ldz, 512)) if K > 256 else None
+            hint = A.gather_hint(4 * min(ldz, 512))  # used by the dwordx4 launches
             call("gcg_spmm_csr_f32_planned_hint", plan.handle, _ptr(A.indptr), _ptr(A.indices),
                  _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(gate), ldg,
                  _ptr(ws), 0 if ws is None else ws.numel() * 4, _ptr(hint), stream)

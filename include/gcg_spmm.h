@@ -144,8 +144,8 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
  * expects to be gathered rarely. Cold rows are gathered with non-temporal loads, so they do not
  * displace the hot rows (hub nodes of a power-law graph) from the L2 / Infinity Cache; the
  * result is bitwise the one without the hint (only the cache policy of the loads changes).
- * Used by the dwordx4 launch of widths 257..512 per column panel (K = 300, 1500); every other
- * launch reads `indices`. graphconvgeo_amd.sparse builds the hint (DeviceCSR.gather_hint).
+ * Used by the dwordx4 launches (K % 4 == 0 with 16-B rows); every other launch reads
+ * `indices`. graphconvgeo_amd.sparse builds the hint (DeviceCSR.gather_hint).
  */
 gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_t* indptr,
                                          const int32_t* indices, const float* vals,

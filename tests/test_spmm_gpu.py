@@ -151,7 +151,7 @@ def test_narrow_rows_subwave_path(cuda, K, mode, monkeypatch):
 
 
 @pytest.mark.parametrize("mode", ["ordered", "fast"])
-@pytest.mark.parametrize("K", [300, 512, 1500])
+@pytest.mark.parametrize("K", [128, 256, 300, 512, 1500])
 def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
     """The gather hint (cold columns' rows gathered non-temporally, DeviceCSR.gather_hint ->
     gcg_spmm_csr_f32_planned_hint) changes the loads' cache policy only: bitwise the hint-less
