@@ -72,14 +72,14 @@ TMATMUL_HEAD_SIDE_STREAM = True
 # larger than the Infinity Cache, the rows of all but the most frequent columns are gathered
 # non-temporally so the hot rows (hub nodes) stay cached. Hot set = the most frequent columns
 # whose gathered rows fit GATHER_HINT_HOT_BYTES; used when they carry >= GATHER_HINT_MIN_SHARE of
-# the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes. Measured on the World
+# the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes (larger than the cache). Measured on the World
 # power-law graph, K = 300 (tools/exp_hot_cold.py, interleaved): hot sets of 12k / 25k / 50k rows
 # (15 / 30 / 61 MB) 6.40 / 6.34 / 6.49 ms vs 6.80 without; every row non-temporal 7.71 vs 6.54;
 # K = 256: 4.96 (16 MB) / 5.10 (32 MB) vs 5.36 ms, K = 128: 2.36 vs 2.43 ms.
 GATHER_HINT = True
 GATHER_HINT_HOT_BYTES = 32 << 20
 GATHER_HINT_MIN_SHARE = 0.25
-GATHER_HINT_MIN_TABLE = 512 << 20
+GATHER_HINT_MIN_TABLE = 256 << 20  # the Infinity Cache (US K = 256, 460 MB: 1.314 -> 1.266 ms)
 
 
 # Integer ids of operators and row lists, for the registered torch ops (graphconvgeo_amd.ops):

@@ -16,6 +16,8 @@ from graphconvgeo_amd.synth import CONFIGS, synthetic_graph  # noqa: E402
 
 dev = torch.device("cuda:0")
 gs.GATHER_HINT = True
+if os.environ.get("HINT_MIN_TABLE_MB"):
+    gs.GATHER_HINT_MIN_TABLE = int(os.environ["HINT_MIN_TABLE_MB"]) << 20
 K = int(os.environ.get("HINT_K", "300"))
 sizes_mb = [int(x) for x in os.environ.get("HINT_MB", "8,16,32,64").split(",")]
 for spec in (sys.argv[1] if len(sys.argv) > 1 else "twitter-world:powerlaw,twitter-us:powerlaw,"
