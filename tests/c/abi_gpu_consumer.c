@@ -173,6 +173,18 @@ int main(void) {
     zeros += pre[i] == 0.0f;
     if (gate[i] != want) { printf("gate differs at %d\n", i); return 28; }
   }
+  /* 4b) the same subset with a gather hint (bit 31 on every other column: non-temporal
+   *     gathers of those rows): the cache policy changes, the bytes do not */
+  int32_t* hint = malloc(sizeof(int32_t) * nnz);
+  for (int i = 0; i < nnz; ++i) hint[i] = (idx[i] & 1) ? (int32_t)((uint32_t)idx[i] | 0x80000000u) : idx[i];
+  int32_t* d_hint;
+  CHECK_HIP(hipMalloc((void**)&d_hint, sizeof(int32_t) * nnz));
+  CHECK_HIP(hipMemcpy(d_hint, hint, sizeof(int32_t) * nnz, hipMemcpyHostToDevice));
+  CHECK_GCG(gcg_spmm_csr_f32_planned_hint(plan, d_ptr, d_idx, d_val, d_Z, K, K, d_Y, K, d_b,
+                                          GCG_ACT_RELU, d_gate, K, NULL, 0, d_hint, st));
+  CHECK_HIP(hipMemcpyAsync(got, d_Y, sizeof(float) * n_sub * K, hipMemcpyDeviceToHost, st));
+  CHECK_HIP(hipStreamSynchronize(st));
+  if (memcmp(got, ref, sizeof(float) * n_sub * K) != 0) { printf("hinted subset differs\n"); return 31; }
   CHECK_GCG(gcg_spmm_plan_destroy(plan));
 
   /* 5) argument errors come back as status codes with a message */
@@ -185,10 +197,11 @@ int main(void) {
 
   CHECK_HIP(hipStreamSynchronize(st));
   hipFree(d_ptr); hipFree(d_idx); hipFree(d_val); hipFree(d_Z); hipFree(d_Y); hipFree(d_b);
-  hipFree(d_rows); hipFree(d_gate); hipFree(d_ws); hipFree(d_status);
+  hipFree(d_rows); hipFree(d_gate); hipFree(d_ws); hipFree(d_status); hipFree(d_hint);
   CHECK_HIP(hipStreamDestroy(st));
-  printf("gpu abi ok: %d rows, %d nnz, K=%d, plan-less/ordered/subset+gate bitwise, "
+  printf("gpu abi ok: %d rows, %d nnz, K=%d, plan-less/ordered/subset+gate(+hint) bitwise, "
          "fast within 1e-4 (%d exact-zero pre-activations)\n", n, nnz, K, zeros);
   free(indptr); free(idx); free(val); free(Z); free(ref); free(got); free(gate); free(pre);
+  free(hint);
   return 0;
 }
