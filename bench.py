@@ -59,28 +59,45 @@ def cpu_model() -> str:
     return platform.processor() or "unknown"
 
 
-def scipy_baseline(H, K: int, reps: int = 3) -> dict:
-    """The reference's own executor over the WHOLE graph: S.dot(H, Z) (mlpconv.py:73) is
-    scipy's `H @ Z` (csr_matvecs, single-threaded whatever the host), here on all nnz(H) of the
-    bench graph against the full N x K float32 operand: 1 warm-up, then the median of `reps`
-    runs (time.perf_counter) -- SURVEY.md §8d."""
+def scipy_baseline(H, K: int, budget_s: float = 30.0) -> dict:
+    """The reference's own executor: S.dot(H, Z) (mlpconv.py:73) is scipy's `H @ Z`
+    (csr_matvecs, single-threaded whatever the host) on the bench graph against the full N x K
+    float32 operand, 1 warm-up then the median of up to 3 runs (time.perf_counter) --
+    SURVEY.md §8d -- bounded by `budget_s`: the whole graph while 4 runs fit the budget
+    (World: ~5.5 s per run on the GPU box's EPYC), else the leading rows that do (the same
+    rows every run; GB/s from that sample's bytes)."""
     import scipy
 
     Z = np.random.default_rng(SEED + 5).standard_normal((H.shape[1], K), dtype=np.float32)
+    # probe ~1/20 of the graph to size the sample
+    n = H.shape[0]
+    stop = int(np.searchsorted(H.indptr, H.nnz // 20, side="left"))
     t0 = time.perf_counter()
-    H @ Z  # warm-up
+    H[:max(stop, 1)] @ Z
+    est = (time.perf_counter() - t0) * H.nnz / max(int(H.indptr[max(stop, 1)]), 1)
+    rows = n
+    if 4 * est > budget_s:  # full graph does not fit: the leading rows that do
+        frac = budget_s / (4 * est)
+        rows = max(1, int(np.searchsorted(H.indptr, int(frac * H.nnz), side="left")))
+    S = H if rows == n else H[:rows]
+    t0 = time.perf_counter()
+    S @ Z  # warm-up
     t_warm = time.perf_counter() - t0
     ts = []
-    for _ in range(max(reps, 3)):
+    for _ in range(3):
+        if ts and sum(ts) + t_warm + ts[-1] > budget_s:
+            break
         t0 = time.perf_counter()
-        H @ Z
+        S @ Z
         ts.append(time.perf_counter() - t0)
     t = float(np.median(ts))
-    return {"value": round(spmm_bytes(H.shape[0], H.nnz, K) / t / 1e9, 3), "unit": "GB/s",
+    what = (f"full graph: all {n} rows" if rows == n else
+            f"rows [0, {rows}) of the same graph (budget {budget_s:.0f} s)")
+    return {"value": round(spmm_bytes(rows, S.nnz, K) / t / 1e9, 3), "unit": "GB/s",
             "cores": 1, "kind": "reference",
-            "edges_per_s": round(H.nnz / t, 1), "seconds_per_spmm": round(t, 3),
-            "sample": f"full graph: scipy {scipy.__version__} H @ Z over all {H.shape[0]} rows "
-                      f"({H.nnz} nnz x K={K}), 1 warm-up ({t_warm:.2f} s) + median of {len(ts)} "
+            "edges_per_s": round(S.nnz / t, 1), "seconds_per_spmm": round(t * H.nnz / S.nnz, 3),
+            "sample": f"{what}: scipy {scipy.__version__} H @ Z ({S.nnz} nnz x K={K}), 1 "
+                      f"warm-up ({t_warm:.2f} s) + median of {len(ts)} "
                       f"({', '.join(f'{x:.2f}' for x in ts)} s), single-threaded scipy "
                       f"csr_matvecs on {cpu_model()} ({os.cpu_count()} host cpus)"}
 
@@ -145,13 +162,24 @@ def cpu_multicore(H, K: int, budget_s: float) -> dict:
             "sample": f"rows [0, {blk.shape[0]}): {blk.nnz} nnz x K={K}, {reps} reps"}
 
 
-PROFILE_ROUNDS = ("r03", "r02", "r01")  # newest first
+PROFILE_ROUNDS = ("r04", "r03", "r02", "r01")  # newest first
+PMC_COUNTERS = ("FETCH_SIZE", "WRITE_SIZE")  # one rocprofv3 pass each (TCC slots, guide §PMC)
+PMC_KERNEL = "spmm_rows_kernel"
+
+
+def library_hash() -> str:
+    """Source hash of the library this run measures (graphconvgeo_amd/_build.source_hash; the
+    binding refuses a library built from other sources, _native._check_fresh)."""
+    from graphconvgeo_amd import _build
+    return _build.source_hash()
 
 
 def load_traffic(workload: str, per_launch_bytes: int):
-    """L2->fabric bytes per launch (FETCH_SIZE x 2 + WRITE_SIZE, the gfx950 correction of
-    MI355X_MICROARCH.md:298; Infinity-Cache hits included, so not DRAM-only bytes) from the
-    newest committed rocprofv3 PMC summary of this workload."""
+    """Fallback when the live PMC pass cannot run: L2->fabric bytes per launch (2 x FETCH_SIZE +
+    WRITE_SIZE, the gfx950 correction of MI355X_MICROARCH.md:298) from the newest committed
+    rocprofv3 PMC summary of this workload -- only one stamped with the source hash of the
+    library this run loads (a summary of another build describes other kernels)."""
+    want = library_hash()
     for rnd in PROFILE_ROUNDS:
         path = os.path.join(ROOT, "profiles", rnd, f"pmc_{workload}.json")
         if not os.path.exists(path):
@@ -159,10 +187,108 @@ def load_traffic(workload: str, per_launch_bytes: int):
         try:
             with open(path) as f:
                 rec = json.load(f)
-            return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
         except (OSError, ValueError):
             continue
+        if rec.get("gcg_source_hash") != want or rec.get("algorithmic_bytes_per_launch") != per_launch_bytes:
+            continue
+        return rec.get("hbm_bytes_per_launch"), os.path.relpath(path, ROOT)
     return None, None
+
+
+def under_profiler() -> bool:
+    """True inside a rocprofv3 run (its tool library is preloaded): no nested PMC pass."""
+    return "rocprof" in os.environ.get("LD_PRELOAD", "") or any(
+        k.startswith("ROCPROF") for k in os.environ)
+
+
+def _read_counter(d: str, counter: str, kernel: str = PMC_KERNEL):
+    import csv
+    import glob
+    per = {}
+    for fn in glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True):
+        with open(fn) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"] and row["Counter_Name"] == counter:
+                    did = int(row["Dispatch_Id"])
+                    per[did] = per.get(did, 0.0) + float(row["Counter_Value"])
+    return [per[k] for k in sorted(per)]
+
+
+def live_traffic(H, K: int, mode: str, timeout_s: int = 240) -> dict:
+    """HBM-side bytes of the bench's own SpMM launch, measured in this run: tools/pmc_probe.py
+    (same graph, layout, mode and gather hint) under `rocprofv3 --pmc FETCH_SIZE` and
+    `--pmc WRITE_SIZE`, one child process per pass (run before this process touches the GPU),
+    each bounded by `timeout -s KILL`. Per launch: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes;
+    the gfx950 correction of MI355X_MICROARCH.md:298), the mean over the launches after the
+    plan-building one. These are L2->fabric bytes: reads the Infinity Cache serves are counted
+    too (no gfx950 TCC counter separates them), so they bound the DRAM bytes from
+    above."""
+    import shutil
+    import subprocess
+    import tempfile
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return {"error": "rocprofv3 not found"}
+    tmpd = tempfile.mkdtemp(prefix="gcg_pmc_")
+    t0 = time.perf_counter()
+    try:
+        graph = os.path.join(tmpd, "graph.npz")
+        np.savez(graph, n=np.int64(H.shape[0]), indptr=H.indptr, indices=H.indices, data=H.data)
+        vals = {}
+        for c in PMC_COUNTERS:
+            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", c, "--output-format",
+                   "csv", "-d", os.path.join(tmpd, c), "-o", c, "--", sys.executable,
+                   os.path.join(ROOT, "tools", "pmc_probe.py"), graph, "--K", str(K),
+                   "--mode", mode]
+            t1 = time.perf_counter()
+            r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s + 30)
+            print(f"bench: live PMC {c} pass rc={r.returncode} in {time.perf_counter() - t1:.1f} s",
+                  file=sys.stderr, flush=True)
+            if r.returncode != 0:
+                return {"error": f"{c} pass rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+            v = _read_counter(os.path.join(tmpd, c), c)
+            if len(v) < 2:
+                return {"error": f"{c}: {len(v)} {PMC_KERNEL} dispatches in the counter CSV"}
+            vals[c] = v[1:]  # drop the plan-building call's launch
+        fetch = float(np.mean(vals["FETCH_SIZE"]))
+        write = float(np.mean(vals["WRITE_SIZE"]))
+        return {"traffic": int(2 * fetch * 1024 + write * 1024),
+                "FETCH_SIZE_KiB_per_launch": round(fetch, 1),
+                "WRITE_SIZE_KiB_per_launch": round(write, 1),
+                "dispatches": {c: len(v) for c, v in vals.items()},
+                "spread": round(max(max(v) / min(v) for v in vals.values()) - 1, 4),
+                "gcg_source_hash": library_hash(), "pass_s": round(time.perf_counter() - t0, 1)}
+    except (OSError, subprocess.SubprocessError, KeyError, ValueError) as exc:
+        return {"error": repr(exc)[:300]}
+    finally:
+        shutil.rmtree(tmpd, ignore_errors=True)
+
+
+def roofline_record(kbytes: int, k_ms: float, traffic, traffic_src: str, kernel: str) -> dict:
+    """SURVEY.md §8d roofline for the headline kernel. `achieved` / `frac` are the MEASURED
+    bytes (rocprofv3 PMC traffic per launch) over the HIP-event kernel time against the 8 TB/s
+    HBM spec -- a physical rate, <= 1 of peak; the edge-centric algorithmic model (one K-wide
+    row read per nonzero) is kept beside it as `edge_centric_*`: it counts
+    re-reads the Infinity Cache serves, so on the power-law graph it exceeds the peak."""
+    edge = kbytes / (k_ms * 1e-3) / 1e9
+    rec = {"bound": "hbm", "peak": HBM_PEAK_GBS, "unit": "GB/s", "kernel": kernel,
+           "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": kbytes,
+           "edge_centric_achieved": round(edge, 1),
+           "edge_centric_frac": round(edge / HBM_PEAK_GBS, 4)}
+    if traffic:
+        ach = traffic / (k_ms * 1e-3) / 1e9
+        rec.update(achieved=round(ach, 1), frac=round(ach / HBM_PEAK_GBS, 4),
+                   frac_vs_achievable=round(ach / HBM_ACHIEVABLE_GBS, 4),
+                   achieved_kind=("measured bytes per launch (rocprofv3 PMC 2 x FETCH_SIZE + "
+                                  "WRITE_SIZE: L2->fabric, Infinity-Cache hits included) / "
+                                  "HIP-event kernel time"),
+                   traffic=int(traffic), traffic_over_algorithmic=round(traffic / kbytes, 4),
+                   traffic_source=traffic_src)
+    else:  # no measured bytes: the model, labelled as such
+        rec.update(achieved=round(edge, 1), frac=round(edge / HBM_PEAK_GBS, 4),
+                   achieved_kind="edge-centric algorithmic bytes / kernel time (no PMC traffic "
+                                 "measured in this run)", traffic=None)
+    return rec
 
 
 def time_events(fn, reps: int, dev) -> float:
@@ -178,12 +304,22 @@ def time_events(fn, reps: int, dev) -> float:
     return float(np.mean([a.elapsed_time(b) for a, b in evs]))
 
 
-def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev) -> dict:
+def host_mode(H, mode: str) -> str:
+    """The mode 'auto' resolves to for host CSR H (sparse.auto_mode), without a device."""
+    if mode != "auto":
+        return mode
+    lens = np.diff(H.indptr)
+    return gs.auto_mode(H.shape[0], H.nnz, int(lens.max()) if lens.size else 0)
+
+
+def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev, H=None, live=None) -> dict:
     """SURVEY.md §8d second run: the same SpMM on the uniform-degree graph of the same size,
-    where no hub rows are served from the Infinity Cache -- the honest HBM-gather case."""
-    H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
+    where no hub rows are served from the Infinity Cache -- the honest HBM-gather case. `live`:
+    this graph's live PMC pass (live_traffic), run before the process touched the GPU."""
+    if H is None:
+        H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
     A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
-    g = torch.Generator(device=dev).manual_seed(SEED + 11)
+    g = torch.Generator(device=dev).manual_seed(SEED)
     Z = gs.empty_dense(H.shape[0], K, dev).copy_(torch.randn((H.shape[0], K), generator=g, device=dev))
     Y = gs.empty_dense(H.shape[0], K, dev)
     eff = resolve_mode(A, mode)
@@ -192,15 +328,16 @@ def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev) -> dict:
     k_ms = time_events(lambda: gs.spmm(A, Z, out=Y, mode=eff), reps, dev)
     B = spmm_bytes(H.shape[0], H.nnz, K)
     gbs = B / (k_ms * 1e-3) / 1e9
-    wl = f"{cfg.name}-{kind}-k{K}-{eff}"
-    traffic, src = load_traffic(wl, B)
+    if live and "traffic" in live:
+        traffic, src = live["traffic"], "live rocprofv3 --pmc pass of this run (bench.live_traffic)"
+    else:
+        traffic, src = load_traffic(f"{cfg.name}-{kind}-k{K}-{eff}", B)
     rec = {"graph": kind, "mode": eff, "nnz_H": H.nnz, "kernel_ms": round(k_ms, 3),
-           "value": round(gbs, 1), "unit": "GB/s", "edges_per_s": round(H.nnz / (k_ms * 1e-3), 1),
-           "frac": round(gbs / HBM_PEAK_GBS, 4),
-           "frac_vs_achievable": round(gbs / HBM_ACHIEVABLE_GBS, 4),
-           "algorithmic_bytes_per_launch": B, "traffic": traffic}
-    if src:
-        rec["traffic_source"] = src
+           "value": round(gbs, 1), "value_kind": "edge-centric", "unit": "GB/s",
+           "edges_per_s": round(H.nnz / (k_ms * 1e-3), 1),
+           "roofline": roofline_record(B, k_ms, traffic, src, "spmm_rows_kernel")}
+    if live and "error" in live:
+        rec["live_pmc_error"] = live["error"]
     del A, Z, Y
     return rec
 
@@ -380,8 +517,12 @@ def main():
     ap.add_argument("--task-nnz", type=int, default=0)
     ap.add_argument("--ld", type=int, default=0,
                     help="row stride of Z/Y in floats (0 = the library's empty_dense layout)")
-    ap.add_argument("--cpu-budget", type=float, default=6.0,
-                    help="seconds of the C-port CPU extra (the scipy baseline is a fixed sample)")
+    ap.add_argument("--cpu-budget", type=float, default=30.0,
+                    help="seconds of CPU baseline work: the scipy baseline (full graph while "
+                         "it fits, else a row sample) and, up to 1/5 of it, the C-port extra")
+    ap.add_argument("--no-live-pmc", dest="live_pmc", action="store_false",
+                    help="N = 1: skip the live rocprofv3 PMC pass (traffic then comes from a "
+                         "committed summary stamped with this library's source hash, if any)")
     ap.add_argument("--no-variants", dest="variants", action="store_false",
                     help="N = 1: skip the uniform-degree second run")
     ap.add_argument("--no-train-step", dest="train_step", action="store_false",
@@ -409,6 +550,28 @@ def main():
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    cfg = CONFIGS[args.config]
+    K = args.hidden or cfg.hidden
+    t_gen = time.perf_counter()
+    H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=args.graph)
+    t_gen = time.perf_counter() - t_gen
+    N, nnz = H.shape[0], H.nnz
+    B = spmm_bytes(N, nnz, K)
+
+    # Live PMC (N = 1): the headline launch's HBM-side bytes, measured by rocprofv3 child
+    # processes before this process touches the GPU (and for the uniform second run's graph).
+    single = world == 1 and not args.partitioned
+    live = live_u = H_u = None
+    if single and args.live_pmc and args.ld == 0 and args.steps > 0:
+        if under_profiler():
+            live = {"error": "skipped: this run is itself under rocprofv3"}
+        else:
+            live = live_traffic(H, K, host_mode(H, args.mode))
+            if args.variants:
+                H_u = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind="uniform")
+                live_u = live_traffic(H_u, K, host_mode(H_u, args.mode))
+
     dev_index = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
@@ -420,14 +583,6 @@ def main():
             dist.init_process_group("gloo")
         if dist.get_world_size() != world:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
-
-    cfg = CONFIGS[args.config]
-    K = args.hidden or cfg.hidden
-    t_gen = time.perf_counter()
-    H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=args.graph)
-    t_gen = time.perf_counter() - t_gen
-    N, nnz = H.shape[0], H.nnz
-    B = spmm_bytes(N, nnz, K)
 
     gen = torch.Generator(device=dev)
     gen.manual_seed(SEED + rank)
@@ -495,28 +650,22 @@ def main():
                 gs.spmm(part.A, full_k, out=Y, mode=eff, task_nnz=args.task_nnz)
             kstep()
         k_ms = time_events(kstep, args.steps, dev)
-        achieved = kbytes / (k_ms * 1e-3) / 1e9
-        workload = f"{args.config}-{args.graph}-k{K}-{eff}"
-        traffic, traffic_src = load_traffic(workload, B) if kbytes == B else (None, None)
-        roofline = {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS,
-                    "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                    "frac_vs_achievable": round(achieved / HBM_ACHIEVABLE_GBS, 4),
-                    "achieved_kind": "edge-centric algorithmic bytes (SURVEY.md §8d) / kernel "
-                                     "time; on the power-law graph hub rows are re-served from "
-                                     "the Infinity Cache, see variants.uniform for the "
-                                     "HBM-gather case",
-                    "traffic": traffic,
-                    "traffic_kind": "L2->fabric bytes per launch (2 x FETCH_SIZE + WRITE_SIZE); "
-                                    "Infinity-Cache hits included (MI355X_MICROARCH.md:297)",
-                    "kernel": "spmm_rows_kernel (+ spmm_fixup_kernel)",
-                    "kernel_ms": round(k_ms, 3), "algorithmic_bytes_per_launch": kbytes,
-                    # compulsory bytes (every array touched once) beside the
-                    # edge-centric count, so cache reuse on the gather is visible
-                    "compulsory_bytes_per_launch": (
-                        compulsory_bytes(N, nnz, K, N) if kbytes == B else
-                        compulsory_bytes(part.n_local, part.nnz_local, K, part.operand_rows()))}
-        if traffic_src:
-            roofline["traffic_source"] = traffic_src
+        traffic = traffic_src = None
+        if kbytes == B:
+            if live and "traffic" in live:
+                traffic = live["traffic"]
+                traffic_src = "live rocprofv3 --pmc pass of this run (bench.live_traffic)"
+            else:
+                traffic, traffic_src = load_traffic(f"{args.config}-{args.graph}-k{K}-{eff}", B)
+        roofline = roofline_record(kbytes, k_ms, traffic, traffic_src,
+                                   "spmm_rows_kernel (+ spmm_fixup_kernel)")
+        if live:
+            roofline["live_pmc"] = live
+        # compulsory bytes (every array touched once) beside the edge-centric
+        # count, so cache reuse on the gather is visible
+        roofline["compulsory_bytes_per_launch"] = (
+            compulsory_bytes(N, nnz, K, N) if kbytes == B else
+            compulsory_bytes(part.n_local, part.nnz_local, K, part.operand_rows()))
         if 4 * K * N <= 256 * 2**20:  # the dense operand fits the Infinity Cache
             roofline["note"] = "cache-resident, not roofline-bound (Z fits the 256 MB Infinity Cache)"
         if kbytes != B:
@@ -579,7 +728,11 @@ def main():
     value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
-        "value": round(value), "unit": "GB/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value), "unit": "GB/s",
+        # value = SURVEY.md §8d's edge-centric algorithmic bytes per step / step time (the
+        # metric's model; it counts re-reads the Infinity Cache serves); the measured HBM-side
+        # rate and its fraction of peak are roofline.achieved / roofline.frac
+        "value_kind": "edge-centric", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "f32", "data": "synthetic",
         "edges_per_s": round(nnz / (ms * 1e-3)),
@@ -602,7 +755,8 @@ def main():
         # SURVEY.md §8d second run: uniform degrees (no Infinity-Cache hub reuse)
         del Z, Y
         rec["variants"] = {"uniform": spmm_variant(cfg, "uniform", K, args.mode,
-                                                   max(args.steps, 5), dev)}
+                                                   max(args.steps, 5), dev, H=H_u, live=live_u)}
+        H_u = None
         if args.graph == "powerlaw" and K != 1500:
             rec["variants"]["k1500"] = spmm_wide_variant(A, N, nnz, 1500, eff,
                                                          max(args.steps // 4, 3), dev)
@@ -617,8 +771,8 @@ def main():
         # BASELINE config 3: Twitter-US 2-layer fwd+bwd step (both layer-2 orders)
         rec["train_step"] = train_step_bench(max(args.steps // 2, 5), max(args.warmup, 2), dev)
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        rec["cpu_baseline"] = scipy_baseline(H, K)
-        rec["cpu_port"] = cpu_baseline(H, K, args.cpu_budget)
+        rec["cpu_baseline"] = scipy_baseline(H, K, args.cpu_budget)
+        rec["cpu_port"] = cpu_baseline(H, K, args.cpu_budget / 5)
         try:
             rec["cpu_multicore"] = cpu_multicore(H, K, min(args.cpu_budget, 5.0))
         except Exception as exc:  # informational only

@@ -137,6 +137,44 @@ __device__ __forceinline__ void store_gate(uint8_t* __restrict__ p, const Vec<VE
   }
 }
 
+// Masked last vector (round 4, TL = 1): a width K that is not a multiple of VEC still runs the
+// VEC-wide gathers when Z's rows are padded to a multiple of VEC (empty_dense: K = 930 -> 932
+// floats). The last vector of a row reads Z's padding columns [K, roundVEC(K)) -- products
+// that are never stored -- while bias loads, Y stores and gate bytes past K are masked.
+// Full vectors (c + VEC <= K) take the plain path; TL = 0 compiles exactly the old code.
+template <int VEC, int TL>
+__device__ __forceinline__ Vec<VEC> load_bias(const float* __restrict__ b, int c, int K) {
+  if (!TL || c + VEC <= K) return load_vec<VEC>(b + c);
+  Vec<VEC> r;
+#pragma unroll
+  for (int q = 0; q < VEC; ++q) r.x[q] = c + q < K ? b[c + q] : 0.0f;
+  return r;
+}
+
+template <int VEC, int TL>
+__device__ __forceinline__ void store_out(float* __restrict__ yrow, int c, int K,
+                                          const Vec<VEC>& v, int nt) {
+  if (!TL || c + VEC <= K) {
+    if (nt)
+      store_vec_nt<VEC>(yrow + c, v);
+    else
+      store_vec<VEC>(yrow + c, v);
+    return;
+  }
+#pragma unroll
+  for (int q = 0; q < VEC; ++q)
+    if (c + q < K) yrow[c + q] = v.x[q];
+}
+
+template <int VEC, int TL>
+__device__ __forceinline__ void store_gate_t(uint8_t* __restrict__ grow, int c, int K,
+                                             const Vec<VEC>& v) {
+  if (!TL || c + VEC <= K) return store_gate<VEC>(grow + c, v);
+#pragma unroll
+  for (int q = 0; q < VEC; ++q)
+    if (c + q < K) grow[c + q] = static_cast<uint8_t>(gate_code(v.x[q]));
+}
+
 // Accumulate nonzeros [s, e) of one row into acc, storage order, U gathers in flight.
 template <int VEC, int NCH, int U, int HC = 0>
 __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __restrict__ indices,
@@ -307,14 +345,14 @@ __device__ __forceinline__ void lds_handover_barrier() {
 // the one the single-wave loop makes, in the same order: bitwise equal (scipy csr_matvecs).
 // A wave issues its next batch's gathers right after its own hand-over, so they fly while the
 // later waves of this batch add. LDS: one row sum (<= 512 floats).
-template <int VEC, int NCH, int U, int WPB, int HC = 0>
+template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
 __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
                                          const int32_t* __restrict__ indices,
                                          const float* __restrict__ vals,
                                          const int32_t* __restrict__ out_rows,
                                          const float* __restrict__ Z, int64_t ldz,
                                          const int (&col)[NCH], const int (&gcol)[NCH],
-                                         const bool (&on)[NCH], float* __restrict__ Y,
+                                         const bool (&on)[NCH], int K, float* __restrict__ Y,
                                          int64_t ldy, const float* __restrict__ bias, int act,
                                          uint8_t* __restrict__ gate, int64_t ldgate,
                                          float* __restrict__ sacc) {
@@ -430,14 +468,14 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
     if (!on[k]) continue;
     Vec<VEC> a = *reinterpret_cast<const Vec<VEC>*>(sacc + (k * kWave + lane) * VEC);
     if (bias != nullptr) {
-      const Vec<VEC> bv = load_vec<VEC>(bias + col[k]);
+      const Vec<VEC> bv = load_bias<VEC, TL>(bias, col[k], K);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) a.x[q] = a.x[q] + bv.x[q];
     }
-    if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], a);
+    if (gate != nullptr) store_gate_t<VEC, TL>(gate + static_cast<int64_t>(p) * ldgate, col[k], K, a);
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.x[q] = apply_act(a.x[q], act);
-    store_vec<VEC>(yrow + col[k], a);
+    store_out<VEC, TL>(yrow, col[k], K, a, 0);
   }
 }
 
@@ -447,7 +485,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
 // The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
 // (coop_row); the other tasks one wave each, in the blocks after them.
-template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0>
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0, int TL = 0>
 __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int4* __restrict__ tasks, int n_tasks, int n_coop, int n_out,
     const int32_t* __restrict__ indptr,
@@ -478,8 +516,9 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
   }
   if (blk < n_coop) {  // a whole-workgroup long row (uniform across the block)
     __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
-    coop_row<VEC, NCH, U, WPB, HC>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z, ldz,
-                               col, gcol, on, Y, ldy, bias, act, gate, ldgate, sacc);
+    coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z,
+                                       ldz, col, gcol, on, K, Y, ldy, bias, act, gate, ldgate,
+                                       sacc);
     return;
   }
   const int w = uniform(n_coop + (blk - n_coop) * WPB + (threadIdx.x >> 6));
@@ -517,7 +556,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     Vec<4> sbv;
 #pragma unroll
     for (int q = 0; q < 4; ++q) sbv.x[q] = 0.0f;
-    if (bias != nullptr) sbv = load_vec<4>(bias + sgcol);
+    if (bias != nullptr) sbv = load_bias<4, TL>(bias, sgcol, K);
     for (int pb = t.x; pb < t.y; pb += SUB) {
       const int p = pb + g;
       const bool live = p < t.y;
@@ -538,14 +577,10 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
 #pragma unroll
         for (int q = 0; q < 4; ++q) acc.x[q] = acc.x[q] + sbv.x[q];
       }
-      if (gate != nullptr) store_gate<4>(gate + static_cast<int64_t>(p) * ldgate + scol, acc);
+      if (gate != nullptr) store_gate_t<4, TL>(gate + static_cast<int64_t>(p) * ldgate, scol, K, acc);
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc.x[q] = apply_act(acc.x[q], act);
-      float* yrow = Y + static_cast<int64_t>(p) * ldy + scol;
-      if (nt_store)
-        store_vec_nt<4>(yrow, acc);
-      else
-        store_vec<4>(yrow, acc);
+      store_out<4, TL>(Y + static_cast<int64_t>(p) * ldy, scol, K, acc, nt_store);
     }
     return;
   }
@@ -557,7 +592,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
     if (bias != nullptr) {
-      bv[k] = load_vec<VEC>(bias + gcol[k]);
+      bv[k] = load_bias<VEC, TL>(bias, gcol[k], K);
     } else {
 #pragma unroll
       for (int q = 0; q < VEC; ++q) bv[k].x[q] = 0.0f;
@@ -581,13 +616,11 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
 #pragma unroll
         for (int q = 0; q < VEC; ++q) acc[k].x[q] = acc[k].x[q] + bv[k].x[q];
       }
-      if (gate != nullptr) store_gate<VEC>(gate + static_cast<int64_t>(p) * ldgate + col[k], acc[k]);
+      if (gate != nullptr)
+        store_gate_t<VEC, TL>(gate + static_cast<int64_t>(p) * ldgate, col[k], K, acc[k]);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = apply_act(acc[k].x[q], act);
-      if (nt_store)
-        store_vec_nt<VEC>(yrow + col[k], acc[k]);
-      else
-        store_vec<VEC>(yrow + col[k], acc[k]);
+      store_out<VEC, TL>(yrow, col[k], K, acc[k], nt_store);
     }
   }
 }
@@ -641,6 +674,8 @@ struct LaunchArgs {
   // gather hint: the column indices with a cold-column sign bit (nullable); used by the
   // dwordx4 launches (NCH 1 and 2), every other launch reads `indices`
   const int32_t* hint = nullptr;
+  // K % VEC != 0 on VEC-padded rows: the last vector of a row is masked (TL = 1 kernels)
+  int tail = 0;
 };
 
 template <int VEC, int NCH, int U, int WPB, int SUB = 1, int HC = 0>
@@ -650,6 +685,15 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   const dim3 grid(a.n_coop + (n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
   static const int xcd = env_int("GCG_XCD_REMAP");
   const int nts = env_int("GCG_SPMM_NT_STORE");
+  if constexpr (VEC == 4) {
+    if (a.tail) {
+      hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 1>), grid, dim3(kWave * WPB),
+                         0, stream, a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices,
+                         a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws,
+                         a.ldws, xcd, a.gate, a.ldgate, nts);
+      return;
+    }
+  }
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows,
                      a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate,
@@ -713,14 +757,26 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   launch_rows_f<VEC, NCH, 64>(a, n_panels, stream);
 }
 
+// Vector width of the gathers. K % 4 != 0 on rows padded to a multiple of 4 floats (ldz % 4 == 0
+// implies ldz >= round4(K): the last vector's padding columns are inside the row) runs dwordx4
+// with a masked last vector (*tail = 1) instead of dwordx2 / dword gathers. Measured before
+// (profiles/r03/spmm_k_odd.jsonl, World): C = 930 uniform 29.6 ms as dwordx2 vs 26.5 ms for the
+// 932-wide dwordx4 product on the same rows. GCG_SPMM_NO_TAIL = 1 restores the old choice (A/B).
 int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
-             const float* bias, const float* ws, int64_t ldws) {
+             const float* bias, const float* ws, int64_t ldws, int* tail) {
+  static const int no_tail = env_int("GCG_SPMM_NO_TAIL");
+  *tail = 0;
   for (int vec : {4, 2}) {
     const size_t bytes = sizeof(float) * vec;
-    if (K % vec == 0 && ldz % vec == 0 && ldy % vec == 0 && aligned(Z, bytes) &&
-        aligned(Y, bytes) && (bias == nullptr || aligned(bias, bytes)) &&
-        (ws == nullptr || (aligned(ws, bytes) && ldws % vec == 0)))
-      return vec;
+    if (ldz % vec == 0 && ldy % vec == 0 && aligned(Z, bytes) && aligned(Y, bytes) &&
+        (bias == nullptr || aligned(bias, bytes)) &&
+        (ws == nullptr || (aligned(ws, bytes) && ldws % vec == 0))) {
+      if (K % vec == 0) return vec;
+      if (vec == 4 && !no_tail) {
+        *tail = 1;
+        return 4;
+      }
+    }
   }
   return 1;
 }
@@ -947,8 +1003,8 @@ gcg_status gcg_spmm_csr_f32_gate(int64_t n_rows, int64_t n_cols, int64_t nnz,
   if (n_out == 0 || K == 0) return GCG_OK;
   LaunchArgs a{nullptr, int(n_out), indptr, indices, vals, out_rows, Z, ldz, int(K), Y, ldy,
                bias, act, nullptr, 0, 0, gate, ldgate};
-  return launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, nullptr, 0),
-                     static_cast<hipStream_t>(stream));
+  const int vec = pick_vec(Z, ldz, Y, ldy, K, bias, nullptr, 0, &a.tail);
+  return launch_spmm(a, vec, static_cast<hipStream_t>(stream));
 }
 
 gcg_status gcg_spmm_plan_host(int64_t n_rows, const int32_t* indptr_host,
@@ -1103,7 +1159,8 @@ gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
                Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate, plan->n_coop,
                gather_hint};
-  if (gcg_status s = launch_spmm(a, pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws), st)) return s;
+  const int vec = pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws, &a.tail);
+  if (gcg_status s = launch_spmm(a, vec, st)) return s;
   if (plan->n_long > 0) {
     const dim3 grid((plan->n_long + kWavesPerBlock - 1) / kWavesPerBlock, (K + kWave - 1) / kWave);
     hipLaunchKernelGGL(spmm_fixup_kernel, grid, dim3(kBlock), 0, st, plan->longs, plan->n_long,

@@ -15,6 +15,7 @@ import ctypes as C
 import hashlib
 import itertools
 import math
+import os
 import weakref
 from typing import Optional, Union
 
@@ -466,6 +467,17 @@ def _check_dense(Z: torch.Tensor, A: DeviceCSR):
     return Z
 
 
+def _gathers_vec4(Z, ldz: int, Y, ldy: int, K: int, bias) -> bool:
+    """Whether the SpMM launch gathers 16-B vectors (spmm.hip pick_vec): ldz, ldy multiples of
+    4 floats, 16-B aligned Z / Y / bias. Since round 4 any K (a masked last vector when
+    K % 4 != 0, unless GCG_SPMM_NO_TAIL=1)."""
+    if ldz % 4 or ldy % 4 or Z.data_ptr() % 16 or Y.data_ptr() % 16:
+        return False
+    if bias is not None and bias.data_ptr() % 16:
+        return False
+    return K % 4 == 0 or os.environ.get("GCG_SPMM_NO_TAIL", "0") in ("", "0")
+
+
 def row_stride(k: int) -> int:
     """Row stride (floats) of empty_dense's k-column rows: a multiple of 4 (16-B aligned rows,
     dwordx4 loads / stores whatever k is), and among those the smallest whose row starts keep a
@@ -594,7 +606,10 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
         else:
             plan = A.plan(sel, ordered=(mode == "ordered"), task_nnz=task_nnz)
             ws = plan.workspace(K)
-            hint = A.gather_hint(4 * min(ldz, 512))  # used by the dwordx4 launches
+            # the hint is read by the dwordx4 launches only (spmm.hip pick_vec): never built
+            # or looked up for a call that gathers narrower vectors
+            hint = A.gather_hint(4 * min(ldz, 512)) if _gathers_vec4(Z, ldz, out, ldy, K, bias) \
+                else None
             call("gcg_spmm_csr_f32_planned_hint", plan.handle, _ptr(A.indptr), _ptr(A.indices),
                  _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc, _ptr(gate), ldg,
                  _ptr(ws), 0 if ws is None else ws.numel() * 4, _ptr(hint), stream)

@@ -77,6 +77,11 @@ const char* gcg_last_error(void);
  * n_out == n_rows when out_rows == NULL. Bitwise equal to scipy float32 `H @ Z`
  * (rows re-indexed by out_rows). Replaces S.dot at mlpconv.py:71,73,90 and the
  * row gather at mlpconv.py:94. The CSR must be valid (see gcg_csr_validate).
+ * Vector width: 16-B gathers when ldz % 4 == 0, ldy % 4 == 0 and Z / Y / bias are 16-B
+ * aligned. When K % 4 != 0 they still are (round 4): the last vector of a row also READS Z's
+ * columns [K, round4(K)) -- inside the row, since ldz % 4 == 0 means ldz >= round4(K), and
+ * never used -- so Z's buffer must extend to column round4(K) of its last row (any [n, ldz]
+ * allocation does); bias, Y and gate are never touched past column K.
  */
 gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
                             const int32_t* indptr, const int32_t* indices,
@@ -144,8 +149,9 @@ gcg_status gcg_spmm_csr_f32_planned_gate(const gcg_spmm_plan* plan, const int32_
  * expects to be gathered rarely. Cold rows are gathered with non-temporal loads, so they do not
  * displace the hot rows (hub nodes of a power-law graph) from the L2 / Infinity Cache; the
  * result is bitwise the one without the hint (only the cache policy of the loads changes).
- * Used by the dwordx4 launches (K % 4 == 0 with 16-B rows); every other launch reads
- * `indices`. graphconvgeo_amd.sparse builds the hint (DeviceCSR.gather_hint).
+ * Used by the dwordx4 launches of up to 512 columns per panel (ldz % 4 == 0 and 16-B aligned
+ * Z / Y / bias, any K); every other launch reads `indices`. graphconvgeo_amd.sparse builds the
+ * hint (DeviceCSR.gather_hint).
  */
 gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_t* indptr,
                                          const int32_t* indices, const float* vals,
@@ -359,7 +365,8 @@ gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
  * scale_dev (nullable, device): multiplies scale (the upstream gradient of the loss, read
  * on the device so the call can sit inside a captured HIP graph). The logits never reach HBM.
  * out needs ldo % 4 == 0 and a 16-B aligned base; its padding columns [N, round4(N)) are
- * written with zeros (whole dwordx4 row stores).
+ * written with zeros (whole dwordx4 row stores). W's padding columns [N, ldw) may hold
+ * anything (NaN included): they never reach a logit.
  */
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
                                         int64_t lda, const float* W, int64_t ldw,

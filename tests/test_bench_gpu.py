@@ -40,7 +40,12 @@ def test_bench_single_gpu_line(cuda):
         assert key in rec, key
     assert rec["n_gpus"] == 1 and rec["steps"] == 3 and rec["warmup"] == 1
     rf = rec["roofline"]
-    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rf["frac_vs_achievable"] > 0
+    assert rf["bound"] == "hbm" and rf["unit"] == "GB/s" and rec["value_kind"] == "edge-centric"
+    # the live PMC pass ran (rocprofv3 child processes): frac is measured bytes / kernel time
+    assert "traffic" in rf["live_pmc"], rf["live_pmc"]
+    assert rf["traffic"] == rf["live_pmc"]["traffic"] > 0 and 0 < rf["frac"] <= 1
+    assert rf["edge_centric_achieved"] > 0 and rf["frac_vs_achievable"] > 0
+    assert rec["variants"]["uniform"]["roofline"]["traffic"] > 0
     assert rec["variants"]["uniform"]["kernel_ms"] > 0 and rec["variants"]["k1500"]["kernel_ms"] > 0
     # the like-for-like point of the scaling series: the same SpMM in the mode N > 1 runs
     if not rec["config"]["mode"].endswith("fast"):

@@ -116,6 +116,32 @@ def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
     assert torch.equal(loss, loss2)
 
 
+@pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (20, 3, 61), (9, 4, 522),
+                                   (40, 50, 300)])
+def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N):
+    """W's padding columns [N, ldw) may hold anything (gcg_spmm.h): NaN there must not reach
+    the softmax sum, the loss or the gradient -- bitwise the zero-padded result."""
+    P, W, b = _rand((M, K), 31, 0.3), _rand((K, N), 32, 0.3), _rand((N,), 33)
+    y = np.random.default_rng(34).integers(0, N, M).astype(np.int32)
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    ldw = (N + 3) // 4 * 4 + 4
+    outs = []
+    for fill in (0.0, float("nan"), float("inf")):
+        Wp = torch.full((K, ldw), fill, device=cuda)
+        Wp[:, :N] = Wt
+        G = empty_dense(M, N, cuda)
+        loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+        dense._fused(Pt, Wp[:, :N], bt, yt, 1.0 / M, None, G, loss, hits)
+        probs = torch.empty_like(G)
+        dense._fused(Pt, Wp[:, :N], bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None)
+        outs.append((G, loss, hits, probs))
+    assert torch.isfinite(outs[0][0]).all() and torch.isfinite(outs[0][1]).all()
+    for o in outs[1:]:
+        for a, ref in zip(o, outs[0]):
+            assert torch.equal(a, ref)
+
+
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (300, 300, 256), (513, 300, 930), (70, 33, 1024),
                                    (40, 50, 300), (33, 70, 700), (65, 17, 900)])
 def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):

@@ -36,6 +36,30 @@ def test_sampled_rows_bitwise(big):
     assert np.array_equal(Y[torch.as_tensor(rows, device=Y.device)].cpu().numpy(), ref)
 
 
+def test_bench_layout_bitwise(big):
+    """The exact launch bench.py times for its headline (bench.py main, N = 1): Z and Y from
+    empty_dense (row stride 304 at K = 300), mode 'auto' (-> ordered on the power-law graph),
+    the default gather hint (built and used at full size: the hinted kernel runs), every hub row
+    and a row sample bitwise the oracle."""
+    cfg, H, A, Z = big
+    Zb = gs.empty_dense(cfg.n_nodes, cfg.hidden, Z.device).copy_(Z)
+    Yb = gs.empty_dense(cfg.n_nodes, cfg.hidden, Z.device)
+    assert Zb.stride(0) == gs.row_stride(cfg.hidden) == 304
+    assert gs.resolve_auto(A) == "ordered"
+    gs.spmm(A, Zb, out=Yb, mode="auto")
+    hint = A.gather_hint(4 * min(Zb.stride(0), 512))
+    assert hint is not None and int((hint < 0).sum()) > 0  # the headline runs the hinted kernel
+    lens = np.diff(H.indptr)
+    rows = np.unique(np.concatenate([
+        np.random.default_rng(1).integers(0, cfg.n_nodes, 3000),
+        np.argsort(lens)[-200:],          # every cooperative hub row and more
+        [0, cfg.n_nodes - 1]]))
+    ref = O.spmm_f32(H, Z.cpu().numpy(), rows=rows)
+    assert np.array_equal(Yb[torch.as_tensor(rows, device=Yb.device)].cpu().numpy(), ref)
+    # and the whole output equals the ordered product on unpadded 1200-B rows (another hot set)
+    assert torch.equal(Yb, gs.spmm(A, Z, mode="ordered"))
+
+
 def test_fast_vs_ordered_and_checksums(big):
     cfg, H, A, Z = big
     Yo = gs.spmm(A, Z, mode="ordered")

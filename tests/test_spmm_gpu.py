@@ -62,6 +62,47 @@ def test_bitwise_vs_oracle(cuda, K, mode):
     assert np.array_equal(Y, ref), np.abs(Y - ref).max()
 
 
+@pytest.mark.parametrize("K", [1, 3, 63, 65, 129, 301, 513, 930])
+@pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
+def test_masked_tail_vec4_bitwise(cuda, K, mode, monkeypatch):
+    """K % 4 != 0 on rows padded to a multiple of 4 floats (empty_dense; C = 930 -> 932): dwordx4
+    gathers with a masked last vector (spmm.hip TL = 1). Bitwise equal to the narrower gathers
+    (GCG_SPMM_NO_TAIL=1) and to the oracle, with bias + rectify + gate bytes, a row subset with
+    duplicates, cooperative hub rows (ordered) and split rows (fast); Y's and the gate's padding
+    columns are never written."""
+    H = rand_csr(700, 900, 12, seed=K, long_rows=[(5, 4500), (600, 1500)])
+    Z = np.random.default_rng(K).standard_normal((900, K)).astype(np.float32)
+    b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
+    rows = np.random.default_rng(6).integers(0, 700, size=300).astype(np.int32)
+    rows[:4] = 5
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    Zd = gs.empty_dense(900, K, cuda).copy_(to_dev(Z, cuda))
+    Zd.as_strided((900, Zd.stride(0)), (Zd.stride(0), 1))[:, K:] = float("nan")  # padding
+    bd = to_dev(b, cuda)
+    outs = {}
+    for no_tail in ("1", "0"):
+        monkeypatch.setenv("GCG_SPMM_NO_TAIL", no_tail)
+        Y = gs.empty_dense(700, K, cuda)
+        Yfull = Y.as_strided((700, Y.stride(0)), (Y.stride(0), 1))
+        Yfull.fill_(7.0)
+        gate = gs.empty_gate(700, K, cuda)
+        gfull = gate.as_strided((700, gate.stride(0)), (gate.stride(0), 1))
+        gfull.fill_(9)
+        gs.spmm(A, Zd, bias=bd, act="relu", mode=mode, gate=gate, out=Y, task_nnz=256)
+        Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
+        assert torch.all(Yfull[:, K:] == 7.0) and torch.all(gfull[:, K:] == 9)
+        outs[no_tail] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
+    for a, c in zip(outs["0"], outs["1"]):
+        assert np.array_equal(a, c)
+    Y, gate, Ys = outs["0"]
+    if mode == "fast":
+        assert np.abs(Y - O.spmm_f32(H, Z, bias=b, act="relu")).max() <= 1e-5
+    else:
+        pre = O.spmm_f32(H, Z, bias=b)
+        assert np.array_equal(Y, O.relu(pre)) and np.array_equal(Ys, O.spmm_f32(H, Z, rows=rows))
+        assert np.array_equal(gate, (2 * (pre > 0) + (pre == 0)).astype(np.uint8))
+
+
 @pytest.mark.parametrize("K", [1, 4, 65, 300, 930])
 @pytest.mark.parametrize("task_nnz", [16, 64, 512])
 def test_fast_mode_tolerance(cuda, K, task_nnz):

@@ -17,7 +17,11 @@ import csv
 import glob
 import json
 import os
+import sys
 from collections import defaultdict
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from graphconvgeo_amd._build import source_hash  # noqa: E402
 
 
 def read_counters(d: str, kernel: str):
@@ -58,6 +62,9 @@ def main():
         "FETCH_SIZE_KiB_per_launch": fetch_kib, "WRITE_SIZE_KiB_per_launch": write_kib,
         "correction": "hbm = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950, MI355X_MICROARCH.md §HBM)",
         "algorithmic_bytes_per_launch": a.bytes,
+        # the library these counters describe (bench.load_traffic refuses another build's):
+        # the tree's source hash, which the loaded library must match (_native._check_fresh)
+        "gcg_source_hash": source_hash(),
     }
     if fetch_kib is not None and write_kib is not None:
         hbm = 2 * fetch_kib * 1024 + write_kib * 1024
