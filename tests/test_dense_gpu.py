@@ -133,7 +133,7 @@ def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N):
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
         dense._fused(Pt, Wp[:, :N], bt, yt, 1.0 / M, None, G, loss, hits)
-        probs = torch.empty_like(G)
+        probs = empty_dense(M, N, cuda)
         dense._fused(Pt, Wp[:, :N], bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None)
         outs.append((G, loss, hits, probs))
     assert torch.isfinite(outs[0][0]).all() and torch.isfinite(outs[0][1]).all()
