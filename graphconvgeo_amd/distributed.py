@@ -30,11 +30,26 @@ import torch
 import torch.distributed as dist
 
 
-def row_partition(indptr: np.ndarray, parts: int, row_cost: int = 2) -> np.ndarray:
-    """Contiguous row blocks with ~equal (nnz + row_cost * rows). Returns bounds[parts+1]."""
+# Partition cost model (round 4). A row longer than HUB_ROW_NNZ nonzeros runs on a whole
+# workgroup in 'ordered' mode (spmm.hip coop_row, 8 x the 512-nnz task) and is bound by ONE CU's
+# gather rate (~19 GB/s for 1216-B rows: 12,189 nonzeros in 0.77 ms), while the bulk of a block
+# spreads over every CU: a hub nonzero costs HUB_WEIGHT bulk nonzeros of the block's time.
+HUB_ROW_NNZ = 4096
+HUB_WEIGHT = 1.0
+
+
+def row_partition(indptr: np.ndarray, parts: int, row_cost: int = 2,
+                  hub_weight: Optional[float] = None, hub_nnz: int = HUB_ROW_NNZ) -> np.ndarray:
+    """Contiguous row blocks with ~equal modelled cost: nnz + row_cost * rows, the nonzeros of
+    rows longer than hub_nnz weighted by hub_weight (default HUB_WEIGHT). Returns bounds[parts+1]."""
     indptr = np.asarray(indptr, dtype=np.int64)
     n = indptr.size - 1
-    cost = indptr + row_cost * np.arange(n + 1, dtype=np.int64)
+    w = HUB_WEIGHT if hub_weight is None else float(hub_weight)
+    lens = np.diff(indptr).astype(np.float64)
+    if w != 1.0:
+        lens = np.where(lens > hub_nnz, lens * w, lens)
+    cost = np.zeros(n + 1, dtype=np.float64)
+    np.cumsum(lens + row_cost, out=cost[1:])
     targets = cost[-1] * np.arange(1, parts, dtype=np.float64) / parts
     cuts = np.searchsorted(cost, targets, side="left")
     bounds = np.concatenate([[0], cuts, [n]]).astype(np.int64)
