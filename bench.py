@@ -530,12 +530,14 @@ def main():
     ap.add_argument("--no-dense", dest="dense", action="store_false",
                     help="N = 1: skip timing the output layer's MFMA kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    # 4 chunks: every N > 1 step is exchange-bound on xGMI, so the exposed
-    # time is ~ exchange + SpMM/chunks x the chunking cost (x1.06 at 2 chunks, x1.26-1.30 at 4)
-    ap.add_argument("--chunks", type=int, default=4,
-                    help="N > 1: column chunks of the all-gather/SpMM pipeline (1 = no overlap)")
-    ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "halo"],
-                    help="N > 1: all-gather every block, or send only the referenced halo rows")
+    # auto chunks: the count minimising a pipeline model of this rank's exchange bytes over
+    # xGMI against its local SpMM, each extra chunk costing the SpMM ~9 %
+    ap.add_argument("--chunks", type=int, default=0,
+                    help="N > 1: column chunks of the exchange/SpMM pipeline (1 = no overlap; "
+                         "0 = auto, RowPartitionedCSR.choose_chunks)")
+    ap.add_argument("--exchange", default="auto", choices=["auto", "allgather", "mesh", "halo"],
+                    help="N > 1: all-gather every block, a direct isend/irecv mesh of whole "
+                         "blocks, or send only the referenced halo rows")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
@@ -605,15 +607,24 @@ def main():
     else:
         from graphconvgeo_amd.distributed import RowPartitionedCSR
         part = RowPartitionedCSR(H, rank, world, dev, exchange=args.exchange)
-        Zl = torch.randn((part.local_block_rows, K), generator=gen, device=dev, dtype=torch.float32)
-        Y = gs.empty_dense(part.n_local, K, dev)
         # one mode for every rank and every N: the whole graph's (RowPartitionedCSR.resolve_mode)
         eff = part.resolve_mode(args.mode)
-        part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
+        chunks = part._n_chunks(args.chunks, K)  # 0 = auto: RowPartitionedCSR.choose_chunks
+        Zl = gs.empty_dense(part.local_block_rows, K, dev).copy_(
+            torch.randn((part.local_block_rows, K), generator=gen, device=dev))
+        Y = gs.empty_dense(part.n_local, K, dev)
+        if world > 1:
+            # the producer's rows live in the exchange buffers' own slots: the step copies
+            # nothing, it is the exchange pipelined with the local SpMM
+            part.chunk_buffers(K, chunks).fill(Zl)
+            step_z = None
+        else:  # world 1: the local SpMM on Zl itself (no exchange, no copies)
+            step_z = Zl
+        part.spmm_pipelined(step_z, Y, n_chunks=chunks, mode=eff, task_nnz=args.task_nnz)
         info = part.A.plan(None, eff == "ordered", args.task_nnz).info() if eff != "rowwise" else {}
 
         def step():
-            part.spmm_pipelined(Zl, Y, n_chunks=args.chunks, mode=eff, task_nnz=args.task_nnz)
+            part.spmm_pipelined(step_z, Y, n_chunks=chunks, mode=eff, task_nnz=args.task_nnz)
 
     def barrier():
         if world > 1:
@@ -703,7 +714,8 @@ def main():
                      "exposed_comm_ms": round(max(ms - t_sp, 0.0), 4),
                      "comm_fraction": round(max(ms - t_sp, 0.0) / ms, 4) if ms > 0 else None,
                      "exchange_inbound_GBps_per_gpu": round(gathered / (t_comm * 1e-3) / 1e9, 1),
-                     "chunks": args.chunks, "rows_local": part.n_local,
+                     "chunks": chunks, "chunks_requested": args.chunks or "auto",
+                     "rows_local": part.n_local,
                      "nnz_local": part.nnz_local, "block_rows": part.block_rows,
                      "spmm_only_aggregate_GBps": round(B / (t_sp * 1e-3) / 1e9, 1)}
 
@@ -724,6 +736,31 @@ def main():
                                     "columns_per_gpu": fp.width, "exchange": "none",
                                     "note": "H replicated (0.34 GB), Z/Y split by columns"}}
         del fp, Zc, Yc
+        # The exchange A/B: the same pipelined step with every exchange --
+        # RCCL all-gather (in place), a direct mesh of isend/irecv pairs (every xGMI link at
+        # once), the halo all-to-all of only the referenced rows -- and each exchange alone.
+        for m in ("allgather", "mesh", "halo"):
+            pm = part if m == part.exchange else RowPartitionedCSR(H, rank, world, dev, exchange=m)
+            cm = pm._n_chunks(args.chunks, K)
+            pm.chunk_buffers(K, cm).fill(Zl)
+            Ym = gs.empty_dense(pm.n_local, K, dev)
+
+            def step_m():
+                pm.spmm_pipelined(None, Ym, n_chunks=cm, mode=eff, task_nnz=args.task_nnz)
+            for _ in range(max(args.warmup, 1)):
+                step_m()
+            t_m = timed(step_m, args.steps)
+            b1 = pm.chunk_buffers(K, 1)
+            b1.fill(Zl)
+            t_x = timed(lambda: pm.layout.exchange(b1.chunks[0][2], async_op=False), reps)
+            alt[f"exchange_{m}_ms"] = round(t_m, 4)
+            alt[f"exchange_{m}"] = {"step_ms": round(t_m, 4), "exchange_alone_ms": round(t_x, 4),
+                                    "chunks": cm, "bytes_in_per_gpu": pm.exchange_bytes_per_row(K),
+                                    "value": round(B / (t_m * 1e-3) / 1e9, 1)}
+            if pm is not part:
+                del pm
+            del Ym
+            torch.cuda.empty_cache()
 
     value = B / (ms * 1e-3) / 1e9
     rec = {

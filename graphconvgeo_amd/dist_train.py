@@ -36,7 +36,7 @@ import torch.distributed as dist
 
 from . import dense
 from . import sparse as gs
-from .distributed import RowPartitionedCSR
+from .distributed import RowPartitionedCSR, TargetRows, local_targets  # noqa: F401 (re-export)
 from .layers import _glorot_uniform, csr_matmul
 from .mlpconv import LasagneAdam
 
@@ -47,13 +47,17 @@ class GPUOps:
     """Rank-local kernels of the partitioned propagate (HIP). Tests inject CPU versions."""
 
     @staticmethod
-    def spmm(A, Z, bias=None, act=None, rows=None, mode="auto", want_gate=False):
-        """Y, or (Y, gate) with the rectify gate bytes (sparse.spmm(gate=...)) if want_gate."""
-        if not want_gate:
-            return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode)
-        n_out = A.n_rows if rows is None else len(rows)
-        gate = gs.empty_gate(n_out, Z.shape[1], A.device)
-        return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode, gate=gate), gate
+    def empty(n: int, K: int, device) -> torch.Tensor:
+        return gs.empty_dense(n, K, device)
+
+    @staticmethod
+    def empty_gate(n: int, K: int, device) -> torch.Tensor:
+        return gs.empty_gate(n, K, device)
+
+    @staticmethod
+    def spmm_into(A, Z, out, bias=None, act=None, rows=None, gate=None, mode="auto"):
+        """out = act(A . Z + bias)[rows] (sparse.spmm), the rectify gate bytes into `gate`."""
+        return gs.spmm(A, Z, bias=bias, act=act, rows=rows, mode=mode, out=out, gate=gate)
 
     @staticmethod
     def relu_backward(gY, gate, bias_grad=True):
@@ -66,6 +70,7 @@ class GPUOps:
 
     @staticmethod
     def scatter_rows(n_rows: int, rows: gs.RowSelection, g: torch.Tensor) -> torch.Tensor:
+        """out[rows[i]] += g[i] into n_rows zero rows, duplicates added in increasing i."""
         from .layers import _index_csr_cached
         full = torch.zeros((n_rows, g.shape[1]), dtype=torch.float32, device=g.device)
         if rows.n:
@@ -75,19 +80,28 @@ class GPUOps:
 
 
 class _PartitionedPropagate(torch.autograd.Function):
-    """Y_p = act(H_p . exchange(Z_p) + b)[rows_p]; dZ_p = H_p . exchange(scatter(g . act'))."""
+    """Y_p = act(H_p . exchange(Z_p) + b)[targets_p], the exchange pipelined with the SpMM over
+    column chunks (distributed.pipelined_product). Backward through H's symmetry:
+      no targets: dZ_p = H_p . exchange(g . act')            (same exchange, same SpMM)
+      targets   : dZ_p = H_p[:, D] . exchange(g_D)           (TargetRowsBackward: only the
+                  distinct targets' gradient rows travel, only their columns are multiplied)"""
 
     @staticmethod
-    def forward(ctx, Z_p, bias, part: RowPartitionedCSR, act, rows, mode, ops):
-        operand = part.all_gather(Z_p.detach())
+    def forward(ctx, Z_p, bias, part: RowPartitionedCSR, act, targets, mode, ops):
+        K = Z_p.shape[1]
+        rows = None if targets is None else targets.rows
+        n_out = part.n_local if rows is None else rows.n
         b = None if bias is None else bias.detach()
         gate = None
         if act == "relu" and any(ctx.needs_input_grad[:2]):
-            Y, gate = ops.spmm(part.A, operand, bias=b, act=act, rows=rows, mode=mode,
-                               want_gate=True)
-        else:
-            Y = ops.spmm(part.A, operand, bias=b, act=act, rows=rows, mode=mode)
-        ctx.part, ctx.act, ctx.rows, ctx.mode, ctx.ops = part, act, rows, mode, ops
+            gate = ops.empty_gate(n_out, K, part.device)
+        Y = ops.empty(n_out, K, part.device)
+
+        def into(A, Z, out, **kw):
+            return ops.spmm_into(A, Z, out, **kw)
+        part.spmm_pipelined(Z_p.detach(), Y, bias=b, gate=gate, act=act, rows=rows, mode=mode,
+                            spmm_into=into)
+        ctx.part, ctx.act, ctx.targets, ctx.mode, ctx.ops = part, act, targets, mode, ops
         ctx.has_bias = bias is not None
         ctx.n_in = Z_p.shape[0]
         ctx.save_for_backward(gate)
@@ -103,11 +117,16 @@ class _PartitionedPropagate(torch.autograd.Function):
             g, g_bias = ctx.ops.relu_backward(gY, gate, bias_grad=want_bias)
         g_Z = None
         if ctx.needs_input_grad[0]:
-            part = ctx.part
-            if ctx.rows is not None:
-                g = ctx.ops.scatter_rows(part.n_local, ctx.rows, g)
-            operand = part.all_gather(g.contiguous())
-            g_Z = ctx.ops.spmm(part.A, operand, mode=ctx.mode)
+            part, ops = ctx.part, ctx.ops
+            g = g.contiguous()
+            if ctx.targets is not None:
+                g_Z = part.target_backward(ctx.targets).backward(g, ops, mode=ctx.mode)
+            else:
+                g_Z = ops.empty(part.n_local, g.shape[1], part.device)
+
+                def into(A, Z, out, **kw):
+                    return ops.spmm_into(A, Z, out, **kw)
+                part.spmm_pipelined(g, g_Z, mode=ctx.mode, spmm_into=into)
             if g_Z.shape[0] != ctx.n_in:  # Z_p was given padded to block_rows (all-gather)
                 pad = torch.zeros((ctx.n_in, g_Z.shape[1]), dtype=g_Z.dtype, device=g_Z.device)
                 pad[: g_Z.shape[0]] = g_Z
@@ -115,41 +134,42 @@ class _PartitionedPropagate(torch.autograd.Function):
         return g_Z, g_bias, None, None, None, None, None
 
 
-def partitioned_propagate(Z_p, part, bias=None, act=None, rows=None, mode="auto", ops=GPUOps):
-    """Differentiable (H . Z + b)[rows] restricted to rank p's rows, Z row-partitioned."""
-    return _PartitionedPropagate.apply(Z_p, bias, part, act, rows, mode, ops)
+def partitioned_propagate(Z_p, part, bias=None, act=None, targets=None, mode="auto", ops=GPUOps):
+    """Differentiable (H . Z + b)[targets] restricted to rank p's rows, Z row-partitioned;
+    targets: None (every local row) or a distributed.TargetRows."""
+    if targets is not None and not isinstance(targets, TargetRows):
+        raise TypeError("targets must be a distributed.TargetRows (every rank's target list)")
+    return _PartitionedPropagate.apply(Z_p, bias, part, act, targets, mode, ops)
 
 
-def local_targets(idx: np.ndarray, start: int, stop: int):
-    """Positions and local row ids of the targets that fall in [start, stop), original order."""
-    idx = np.asarray(idx)
-    pos = np.nonzero((idx >= start) & (idx < stop))[0]
-    return pos, (idx[pos] - start).astype(np.int32)
-
-
-class PartitionTargets:
+class PartitionTargets(TargetRows):
     """One target list (train / dev / test indices, the reference's `target_indices`) split
     over the row partition: rank p keeps the targets in its rows [start, stop), in original
-    order. `rows` are the distinct local rows (increasing) with `weight` their multiplicities
-    (None when no row repeats) and `y` the label of each distinct row; `inverse` maps every kept
-    target to its distinct row, `pos` every kept target to its place in the global list."""
+    order. Default: `rows` are the distinct local rows (increasing) with `weight` their
+    multiplicities (None when no row repeats) and `y` the label of each distinct row (from
+    y_all, the labels of every node); `inverse` maps every kept target to its distinct row, `pos`
+    every kept target to its place in the global list. With y_targets (one label per target of
+    the global list, e.g. accuracy's y_true): every kept target is its own row, with its own
+    label -- duplicates may then disagree (MLPCONV.accuracy compares each target with its own)."""
 
-    def __init__(self, idx, y_all, start: int, stop: int, device):
-        idx = np.asarray(idx)
-        self.idx = idx
-        self.total = int(idx.size)
-        self.pos, loc = local_targets(idx, start, stop)
-        uniq, first, inverse, counts = np.unique(loc, return_index=True, return_inverse=True,
-                                                 return_counts=True)
-        self.inverse = torch.as_tensor(inverse.astype(np.int64), device=device)
-        self.rows = gs.RowSelection(uniq.astype(np.int32), device)
-        self.weight = None if uniq.size == loc.size else \
-            torch.as_tensor(counts.astype(np.float32), device=device)
-        self.y = None if y_all is None else torch.as_tensor(
-            np.asarray(y_all)[idx[self.pos][first]].astype(np.int32), device=device)
-
-    def __len__(self):
-        return int(self.pos.size)
+    def __init__(self, idx, y_all, part: RowPartitionedCSR, device=None, y_targets=None):
+        distinct = y_targets is None
+        super().__init__(idx, part, distinct=distinct)
+        device = part.device if device is None else device
+        n_kept = int(self.pos.size)
+        if distinct:
+            self.inverse = torch.as_tensor(self.inverse_host.astype(np.int64), device=device)
+            self.weight = None if self.counts.size == n_kept else \
+                torch.as_tensor(self.counts.astype(np.float32), device=device)
+            self.y = None if y_all is None else torch.as_tensor(
+                np.asarray(y_all)[self.idx[self.pos][self.first]].astype(np.int32), device=device)
+        else:
+            self.inverse = torch.arange(n_kept, dtype=torch.int64, device=device)
+            self.weight = None
+            y_t = np.asarray(y_targets)
+            if y_t.shape != self.idx.shape:
+                raise ValueError("y_targets must hold one label per target")
+            self.y = torch.as_tensor(y_t[self.pos].astype(np.int32), device=device)
 
 
 class RowPartitionedGCN:
@@ -199,11 +219,12 @@ class RowPartitionedGCN:
         self._bucket = torch.empty(sum(sizes), dtype=torch.float32, device=self.device)
         self._sizes = sizes
 
-    def add_targets(self, name: str, idx, y=None):
+    def add_targets(self, name: str, idx, y=None, y_targets=None):
         """Register a target list (the reference's dev / test indices) under `name`; labels from
-        the y given at construction unless `y` (labels of every node) is passed."""
-        self.targets[name] = PartitionTargets(idx, self._y_all if y is None else y,
-                                              self.part.start, self.part.stop, self.device)
+        the y given at construction unless `y` (labels of every node) or `y_targets` (one label
+        per target, duplicates may differ) is passed."""
+        self.targets[name] = PartitionTargets(idx, self._y_all if y is None else y, self.part,
+                                              self.device, y_targets=y_targets)
 
     @torch.no_grad()
     def broadcast_params(self):
@@ -230,12 +251,12 @@ class RowPartitionedGCN:
         tg = self.targets[name]
         h = self._hidden()
         if self.order == "propagate_first":
-            P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+            P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
             loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, tg.y, denom=tg.total,
                                                row_weight=tg.weight)
         else:
             Z2 = dense.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
-            logits = partitioned_propagate(Z2, self.part, self.b2, None, tg.rows, self.mode)
+            logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode)
             loss, acc = dense.softmax_xent(logits, tg.y, denom=tg.total, row_weight=tg.weight)
         if penalty and self.rank == 0:
             c_out, c_hid = self.regul_coefs  # mlpconv.py:235-243, counted once
@@ -261,15 +282,15 @@ class RowPartitionedGCN:
         tg = self.targets[name]
         h = self._hidden()
         if self.order == "propagate_first" and self.n_classes <= dense.FUSED_MAX_COLS:
-            P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+            P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
             probs = self.proj.probabilities(P, self.W2, self.b2)
         else:
             if self.order == "propagate_first":
-                P = partitioned_propagate(h, self.part, None, None, tg.rows, self.mode)
+                P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
                 logits = dense.matmul(P, self.W2, self.b2)
             else:
                 Z2 = dense.matmul(h, self.W2)
-                logits = partitioned_propagate(Z2, self.part, self.b2, None, tg.rows, self.mode)
+                logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode)
             probs = dense.softmax(logits)
         return probs.index_select(0, tg.inverse)
 
@@ -459,9 +480,9 @@ class RowPartitionedMLPCONV:
         y_true = np.asarray(y_true)
         if y_true.shape != idx.shape:
             raise ValueError("y_true must hold one label per target of the partition")
-        y_all = np.zeros(self.net.part.n, dtype=np.int64)
-        y_all[idx] = y_true
-        self.net.add_targets("_accuracy", idx, y_all)
+        # one label per target (duplicates drawn with replacement may carry different labels:
+        # each is scored against its own, as MLPCONV.accuracy does)
+        self.net.add_targets("_accuracy", idx, y_targets=y_true)
         try:
             _loss, acc = self.net.evaluate("_accuracy", penalty=False)
         finally:

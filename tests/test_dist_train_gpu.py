@@ -62,7 +62,8 @@ def _run(order, exchange, steps=8, world=2):
 
 
 @pytest.mark.parametrize("order,exchange", [("propagate_first", "halo"),
-                                            ("reference", "allgather")])
+                                            ("reference", "allgather"),
+                                            ("propagate_first", "mesh")])
 def test_row_partitioned_training_matches_oracle(cuda, order, exchange):
     from oracle import gcn_oracle as O
     steps = 8
