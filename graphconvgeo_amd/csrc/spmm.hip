@@ -764,7 +764,7 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
 // 932-wide dwordx4 product on the same rows. GCG_SPMM_NO_TAIL = 1 restores the old choice (A/B).
 int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
              const float* bias, const float* ws, int64_t ldws, int* tail) {
-  static const int no_tail = env_int("GCG_SPMM_NO_TAIL");
+  const int no_tail = env_int("GCG_SPMM_NO_TAIL");  // read per call: tests toggle it
   *tail = 0;
   for (int vec : {4, 2}) {
     const size_t bytes = sizeof(float) * vec;

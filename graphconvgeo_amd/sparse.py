@@ -71,14 +71,19 @@ TMATMUL_HEAD_SIDE_STREAM = True
 
 # Gather hint (round 3, DeviceCSR.gather_hint): on a skewed matrix whose dense operand is far
 # larger than the Infinity Cache, the rows of all but the most frequent columns are gathered
-# non-temporally so the hot rows (hub nodes) stay cached. Hot set = the most frequent columns
-# whose gathered rows fit GATHER_HINT_HOT_BYTES; used when they carry >= GATHER_HINT_MIN_SHARE of
-# the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes (larger than the cache). Measured on the World
-# power-law graph, K = 300 (tools/exp_hot_cold.py, interleaved): hot sets of 12k / 25k / 50k rows
-# (15 / 30 / 61 MB) 6.40 / 6.34 / 6.49 ms vs 6.80 without; every row non-temporal 7.71 vs 6.54;
-# K = 256: 4.96 (16 MB) / 5.10 (32 MB) vs 5.36 ms, K = 128: 2.36 vs 2.43 ms.
+# non-temporally so the hot rows (hub nodes) stay cached. Round 4: the hot set comes from the
+# graph's own column-frequency histogram -- every column gathered at least GATHER_HINT_MIN_REUSE
+# times the mean column count -- capped at GATHER_HINT_HOT_BYTES of rows (the 8 XCDs' L2, 8 x 4
+# MiB: hot sets beyond it measured slower); used when the hot set carries >= GATHER_HINT_MIN_SHARE
+# of the nonzeros and the operand is >= GATHER_HINT_MIN_TABLE bytes (larger than the cache).
+# Measured on the power-law graphs, K = 300 (tools/exp_hot_cold.py, interleaved): World hot sets
+# of 8 / 16 / 32 / 64 MiB 6.52 / 6.31 / 6.22 / 6.27 ms vs 6.48 without (4 x the mean count
+# reaches 45 MiB there: capped at 32), Twitter-US 1.60 / 1.565 / 1.57 / 1.61 vs 1.667 (4 x the
+# mean: 15.5 MiB); every row non-temporal 7.71 vs 6.54; the uniform graphs have no column at
+# 4 x the mean (no hint). K = 256: 4.96 (16 MB) / 5.10 (32 MB) vs 5.36 ms, K = 128: 2.36 vs 2.43.
 GATHER_HINT = True
 GATHER_HINT_HOT_BYTES = 32 << 20
+GATHER_HINT_MIN_REUSE = 4.0
 GATHER_HINT_MIN_SHARE = 0.25
 GATHER_HINT_MIN_TABLE = 256 << 20  # the Infinity Cache (US K = 256, 460 MB: 1.314 -> 1.266 ms)
 
@@ -346,27 +351,34 @@ class DeviceCSR:
 
     def gather_hint(self, row_bytes: int) -> Optional[torch.Tensor]:
         """Column indices with bit 31 set on the cold columns (gcg_spmm_csr_f32_planned_hint),
-        or None where the hint does not pay (see GATHER_HINT_*). Built once per hot-set size on
-        the device; the SpMM result does not depend on it (cache policy only)."""
+        or None where the hint does not pay (see GATHER_HINT_*). Built once per row size on the
+        device (one host sync); the SpMM result does not depend on it (cache policy only). A
+        first call inside a HIP-graph capture cannot sync: it returns None (the captured launch
+        then gathers every row with the default policy -- same result) without caching."""
         if not GATHER_HINT or self.nnz == 0:
             return None
-        n_hot = max(1, GATHER_HINT_HOT_BYTES // max(1, row_bytes))
-        if n_hot >= self.n_cols or self.n_cols * row_bytes < GATHER_HINT_MIN_TABLE:
+        n_cap = max(1, GATHER_HINT_HOT_BYTES // max(1, row_bytes))
+        if n_cap >= self.n_cols or self.n_cols * row_bytes < GATHER_HINT_MIN_TABLE:
             return None
         cache = self.__dict__.setdefault("_gather_hints", {})
-        if n_hot not in cache:
+        if n_cap not in cache:
+            if torch.cuda.is_current_stream_capturing():
+                return None
             idx = self.indices.to(torch.int64)
             counts = torch.bincount(idx, minlength=self.n_cols)
-            top = torch.topk(counts, n_hot, sorted=False).indices
+            vals, top = torch.topk(counts, n_cap, sorted=True)
+            thr = GATHER_HINT_MIN_REUSE * self.nnz / self.n_cols
+            n_hot = int((vals >= thr).sum())
             hint = None
-            if float(counts[top].sum()) >= GATHER_HINT_MIN_SHARE * self.nnz:
+            if n_hot and float(vals[:n_hot].sum()) >= GATHER_HINT_MIN_SHARE * self.nnz:
                 hot = torch.zeros(self.n_cols, dtype=torch.bool, device=self.device)
-                hot[top] = True
+                hot[top[:n_hot]] = True
                 cold_bit = torch.tensor(-2 ** 31, dtype=torch.int32, device=self.device)
                 hint = torch.where(hot[idx], self.indices, self.indices | cold_bit)
             del idx, counts
-            cache[n_hot] = hint
-        return cache[n_hot]
+            self._hint_hot_rows = n_hot
+            cache[n_cap] = hint
+        return cache[n_cap]
 
     def _dense_column_split(self):
         """The columns dense enough that A^T . G is cheaper as a dense MFMA product.

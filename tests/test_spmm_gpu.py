@@ -224,6 +224,28 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
         assert np.array_equal(outs["0"][2], O.spmm_f32(H, Z, rows=rows))
 
 
+def test_gather_hint_first_call_inside_capture(cuda, monkeypatch):
+    """A hint first needed inside a HIP-graph capture cannot be built there (its build syncs):
+    the captured launch runs without it (default cache policy, same result) and nothing is
+    cached; the next eager call builds it."""
+    monkeypatch.setattr(gs, "GATHER_HINT", True)
+    monkeypatch.setattr(gs, "GATHER_HINT_MIN_TABLE", 0)
+    monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 4 << 20)
+    H = synthetic_graph(20_000, 200_000)
+    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
+    gs.spmm(A, gs.empty_dense(20_000, 16, cuda).normal_(), mode="ordered")  # plan (outside)
+    Z = gs.empty_dense(20_000, 300, cuda).copy_(to_dev(dense(20_000, 300), cuda))
+    out = gs.empty_dense(20_000, 300, cuda)
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        gs.spmm(A, Z, out=out, mode="ordered")
+    assert 4 * 2**20 // 1216 not in A.__dict__.get("_gather_hints", {})  # not built in the capture
+    g.replay()
+    torch.cuda.synchronize()
+    eager = gs.spmm(A, Z, mode="ordered")  # builds and uses the hint
+    assert A.gather_hint(1216) is not None and torch.equal(out, eager)
+
+
 def test_gather_hint_off_where_it_does_not_pay(cuda, monkeypatch):
     """No hint on a small operand (the Infinity Cache holds it) or a graph without hub columns."""
     monkeypatch.setattr(gs, "GATHER_HINT", True)
