@@ -398,3 +398,70 @@ def test_mode_resolved_once_for_all_ranks():
             b = RowPartitionedCSR(H, q, P, "cpu", local_spmm=_oracle_spmm).bounds
             L = lens[b[q]:b[q + 1]]
             assert m == gs.auto_mode(L.size, int(L.sum()), int(L.max()))
+
+
+def test_chunk_count_model():
+    """RowPartitionedCSR.choose_chunks: 1 with nothing to hide (world 1); the pipeline model's
+    optimum otherwise -- exchange-bound steps take the most chunks, chunks stay >= 64 columns --
+    and pipeline_time itself: 1 chunk = exchange + SpMM, more chunks hide the shorter phase."""
+    from graphconvgeo_amd.distributed import (MAX_CHUNKS, RowPartitionedCSR, pipeline_time)
+    assert pipeline_time(2.0, 1.0, 1) == 3.0
+    assert pipeline_time(2.0, 1.0, 4) < pipeline_time(2.0, 1.0, 2) < 3.0
+    assert pipeline_time(0.0, 1.0, 4) > pipeline_time(0.0, 1.0, 1)  # nothing to hide: chunks cost
+    H = synthetic_graph(20_000, 160_000)
+    one = RowPartitionedCSR(H, 0, 1, "cpu", local_spmm=_oracle_spmm)
+    assert one.choose_chunks(300) == 1
+    p = RowPartitionedCSR(H, 0, 4, "cpu", local_spmm=_oracle_spmm, exchange="allgather")
+    assert p.choose_chunks(300) == MAX_CHUNKS   # the exchange dwarfs a 20k-node local SpMM
+    assert p.choose_chunks(100) == 1            # one 64-column chunk at most
+    assert p.choose_chunks(130) == 2
+    p.chunks_override = 3
+    assert p._n_chunks("auto", 300) == 3 and p._n_chunks(2, 300) == 2
+
+
+def test_row_partition_hub_weight():
+    """The cost model: hub rows (longer than hub_nnz) weighted by hub_weight move the cuts away
+    from the blocks that hold them; weight 1 is the round-3 nnz + 2 * rows balance."""
+    from graphconvgeo_amd.distributed import row_partition
+    lens = np.array([1] * 1000 + [5000] + [1] * 9000)
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    b1 = row_partition(indptr, 2)
+    cost = indptr + 2 * np.arange(indptr.size)
+    assert abs(cost[b1[1]] - cost[-1] / 2) <= 5000 + 3
+    b3 = row_partition(indptr, 2, hub_weight=3.0)
+    assert b3[1] <= b1[1]  # the block holding the hub row gets fewer rows
+    assert row_partition(indptr, 2, hub_weight=1.0).tolist() == b1.tolist()
+
+
+def test_target_rows_backward_operator_structure():
+    """TargetRowsBackward on one rank of a 3-way partition: the operator is H_q with every column
+    outside the global distinct targets dropped, columns remapped to each owner's block of the
+    exchange layout; every rank's distinct targets come from the global list (no communication);
+    the operator times the scattered-then-gathered gradient equals H_q times the full scatter."""
+    from oracle import gcn_oracle as O
+    from graphconvgeo_amd.distributed import RowPartitionedCSR, TargetRows
+    n, e = 3000, 20000
+    H = synthetic_graph(n, e)
+    rng = np.random.default_rng(9)
+    targets = rng.integers(0, 2000, size=1800).astype(np.int32)  # bunched on the first ranks
+    g_full = np.zeros((n, 8), np.float32)
+    G = rng.standard_normal((targets.size, 8)).astype(np.float32)
+    O.scatter_add_f32(g_full, targets, G)
+    for r in range(3):
+        part = RowPartitionedCSR(H, r, 3, "cpu", local_spmm=_oracle_spmm, exchange="allgather")
+        tg = TargetRows(targets, part)
+        op = part.target_backward(tg)
+        assert part.target_backward(tg) is op
+        counts = op.layout.counts
+        assert counts == [np.unique(targets[(targets >= part.bounds[q]) &
+                                            (targets < part.bounds[q + 1])]).size for q in range(3)]
+        # operand: each rank's distinct rows of the scattered gradient, in its block
+        operand = np.zeros((3 * op.layout.pad, 8), np.float32)
+        for q, d in enumerate(tg.block_distinct):
+            operand[q * op.layout.pad:q * op.layout.pad + d.size] = g_full[d]
+        got = O.spmm_f32(op.host, operand)
+        want = O.spmm_f32(H[part.start:part.stop], g_full)
+        assert np.array_equal(got, want)
+        assert op.nnz < part.nnz_local
+    # bunched targets: the exact-count mesh is chosen over the padded all-gather
+    assert op.layout.method == "mesh"
