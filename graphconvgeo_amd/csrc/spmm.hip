@@ -493,7 +493,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
     float* __restrict__ ws, int64_t ldws, int xcd_remap, uint8_t* __restrict__ gate,
-    int64_t ldgate, int nt_store, int panel_base) {
+    int64_t ldgate, int nt_store) {
   // Optional XCD-aware mapping (experiment): blocks b and b + 8 share an XCD under the
   // observed round-robin dispatch, so block b takes task block (b % 8) * ceil(nb / 8) + b / 8
   // and each XCD walks one contiguous range of rows. Placement is speed-only, never correctness.
@@ -504,7 +504,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     blk = (nb % 8 == 0) ? cand : blk;  // bijective only when 8 divides the grid
   }
   const int lane = threadIdx.x & (kWave - 1);
-  const int panel0 = (static_cast<int>(blockIdx.y) + panel_base) * (kWave * VEC * NCH);
+  const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
 
   int col[NCH], gcol[NCH];  // output column / clamped gather column
   bool on[NCH];
@@ -676,7 +676,6 @@ struct LaunchArgs {
   const int32_t* hint = nullptr;
   // K % VEC != 0 on VEC-padded rows: the last vector of a row is masked (TL = 1 kernels)
   int tail = 0;
-  int panel_base = 0;  // first column panel of this launch (grid.y counts from it)
 };
 
 template <int VEC, int NCH, int U, int WPB, int SUB = 1, int HC = 0>
@@ -691,14 +690,14 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
       hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 1>), grid, dim3(kWave * WPB),
                          0, stream, a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices,
                          a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws,
-                         a.ldws, xcd, a.gate, a.ldgate, nts, a.panel_base);
+                         a.ldws, xcd, a.gate, a.ldgate, nts);
       return;
     }
   }
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows,
                      a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate,
-                     a.ldgate, nts, a.panel_base);
+                     a.ldgate, nts);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
@@ -791,8 +790,6 @@ int panel_override() {
   return v;
 }
 
-gcg_status launch_panels(const LaunchArgs& a, int vec, int nch, int n_panels, hipStream_t stream);
-
 gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
   const int64_t K = a.K;
   const int req = panel_override();  // experiment knob: panel width in floats
@@ -806,19 +803,6 @@ gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
   const int panel = per_chunk * nch;
   const int n_panels = static_cast<int>((K + panel - 1) / panel);
   if (a.n_tasks <= 0 || K <= 0) return GCG_OK;
-  if (a.tail && n_panels > 1 && !env_int("GCG_SPMM_TAIL_ONE_LAUNCH")) {
-    // only the last panel holds the masked vector: the full panels run the TL = 0 kernel
-    // (the masked form carries more SGPR spills), the last one alone the TL = 1 kernel
-    LaunchArgs full = a, last = a;
-    full.tail = 0;
-    last.panel_base = n_panels - 1;
-    if (gcg_status s = launch_panels(full, vec, nch, n_panels - 1, stream)) return s;
-    return launch_panels(last, vec, nch, 1, stream);
-  }
-  return launch_panels(a, vec, nch, n_panels, stream);
-}
-
-gcg_status launch_panels(const LaunchArgs& a, int vec, int nch, int n_panels, hipStream_t stream) {
   switch (vec * 16 + nch) {
     case 4 * 16 + 1: launch_rows<4, 1>(a, n_panels, stream); break;
     case 4 * 16 + 2: launch_rows<4, 2>(a, n_panels, stream); break;

@@ -10,10 +10,3 @@ timeout -k 10 400 python -u -m pytest -x -q --tb=short --timeout 300 --timeout-m
 tail -2 $out/tests.log
 timeout -k 10 300 python3 -u tools/exp_nt_persist.py > $out/persist.jsonl 2>&1 || { tail -20 $out/persist.jsonl; exit 1; }
 grep '^{' $out/persist.jsonl
-timeout -k 10 300 python -u -m pytest -x -q --tb=short --timeout 200 --timeout-method thread -m gpu tests/test_spmm_gpu.py -k "tail" > $out/tail_tests.log 2>&1 || { tail -30 $out/tail_tests.log; exit 1; }
-tail -1 $out/tail_tests.log
-for v in split one notail; do
-  e=""; [ $v = one ] && e="GCG_SPMM_TAIL_ONE_LAUNCH=1"; [ $v = notail ] && e="GCG_SPMM_NO_TAIL=1"
-  env $e KS=930,932 timeout -k 10 300 python -u tools/exp_spmm_k.py uniform,powerlaw > $out/tail_$v.jsonl 2>&1 || { tail -10 $out/tail_$v.jsonl; exit 1; }
-  echo "== $v"; grep '^{' $out/tail_$v.jsonl
-done
