@@ -840,51 +840,39 @@ gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t ld
   }
   const int kmax4 = (K - 1) & ~3;
   auto tile_of = [&](int i) { return t_lo + li + i * nl; };
-  // The DMA source rows of the tile being issued, recomputed once per tile (not per chunk:
-  // the divisions and 64-bit row addresses per issue measured 25 % slower).
-  const float* src[NU];
-  int iss_i = 0, iss_c = 0, iss_c0 = 0;  // next chunk to issue: tile, chunk, first column
-  auto set_src = [&](int i) {
+  auto issue = [&](int g) {
+    const int i = g / n_chunks, c = g - i * n_chunks;
     const int tile = tile_of(i);
     const int rt_ = tile / n_col_tiles, ct_ = tile - rt_ * n_col_tiles;
     const int64_t r0 = static_cast<int64_t>(rt_) * BM;
-    iss_c0 = ct_ * BN;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int r = img_row[u];
-      if (r < BM) {
-        const int64_t gr = r0 + r;
-        src[u] = A + (gr < M ? gr : static_cast<int64_t>(M) - 1) * lda;
-      } else {
-        const int rb = r - BM;
-        const int n = iss_c0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
-        src[u] = Bt + static_cast<int64_t>(n < N ? n : N - 1) * ldb;
-      }
-    }
-  };
-  if (my_tiles > 0) set_src(0);
-  auto issue = [&](int g) {  // issues chunk g == the next chunk (iss_i, iss_c)
+    const int c0 = ct_ * BN;
     float* stage = smem + (g % S) * STAGE;
 #pragma unroll
     for (int u = 0; u < NU; ++u) {
       const int ii = wave + Cfg::NW * u;
       if (NU * Cfg::NW != Cfg::NGLDS && ii >= Cfg::NGLDS) break;  // wave-uniform
-      int k = iss_c * KC + kofs[u];
+      const int r = img_row[u];
+      const float* src;
+      if (r < BM) {
+        const int64_t gr = r0 + r;
+        src = A + (gr < M ? gr : static_cast<int64_t>(M) - 1) * lda;
+      } else {
+        const int rb = r - BM;
+        const int n = c0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
+        src = Bt + static_cast<int64_t>(n < N ? n : N - 1) * ldb;
+      }
+      int k = c * KC + kofs[u];
       k = k < kmax4 ? k : kmax4;
-      glds16(src[u] + k, stage + ii * 256);
+      glds16(src + k, stage + ii * 256);
     }
-    if (iss_c == 0 && bias != nullptr && wave == 0) {  // lane l: bias[c0 + l] (0 past N)
+    if (c == 0 && bias != nullptr && wave == 0) {  // lane l: bias[c0 + l] (0 past N)
       const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), static_cast<short>(0),
                                                         N * 4, 0x00020000);
 #pragma unroll
       for (int h = 0; h < BN / 64; ++h)
         __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(sbias + (iss_i & 1) * BN + 64 * h), 4,
-            (iss_c0 + 64 * h + lane) * 4, 0, 0, 0);
-    }
-    if (++iss_c == n_chunks) {
-      iss_c = 0;
-      if (++iss_i < my_tiles) set_src(iss_i);
+            rs, (__attribute__((address_space(3))) void*)(sbias + (i & 1) * BN + 64 * h), 4,
+            (c0 + 64 * h + lane) * 4, 0, 0, 0);
     }
   };
 
@@ -928,7 +916,8 @@ gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t ld
 #pragma unroll
   for (int g = 0; g < S - 1; ++g)
     if (g < total) issue(g);
-  for (int g = 0, i = 0, c = 0; g < total; ++g) {
+  for (int g = 0; g < total; ++g) {
+    const int i = g / n_chunks, c = g - i * n_chunks;
     // (the previous epilogue's stores share the counter: waiting until at most the later
     // chunks' DMA count is outstanding retires this chunk's DMA whatever order loads and
     // stores complete in -- at worst it waits for a store or a later chunk too)
@@ -973,10 +962,6 @@ gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t ld
         for (int gg = 0; gg < G; ++gg)
 #pragma unroll
           for (int e = 0; e < 4; ++e) acc[t][gg][e] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (++c == n_chunks) {
-      c = 0;
-      ++i;
     }
   }
 }
