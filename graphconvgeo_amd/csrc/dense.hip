@@ -790,7 +790,8 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // its workgroups take every (nwg / 8)-th). The DMA ring runs over a chunk counter that spans the
 // workgroup's tiles, so the first S - 1 chunks of tile i+1 are in flight while tile i's last
 // chunks compute and its epilogue stores -- a fresh workgroup per tile starts cold instead.
-// Same per-tile arithmetic and order as gemm_nt_kernel: bitwise equal.
+// The first chunk of every tile after the first waits vmcnt(0) (the epilogue's stores share
+// the counter with the DMA). Same per-tile arithmetic and order as gemm_nt_kernel: bitwise equal.
 template <int RT, int G, int WR, int WC, int S>
 __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S, 16>::OCC)) void
 gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
@@ -918,10 +919,9 @@ gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t ld
     if (g < total) issue(g);
   for (int g = 0; g < total; ++g) {
     const int i = g / n_chunks, c = g - i * n_chunks;
-    // (the previous epilogue's stores share the counter: waiting until at most the later
-    // chunks' DMA count is outstanding retires this chunk's DMA whatever order loads and
-    // stores complete in -- at worst it waits for a store or a later chunk too)
-    if (g + S - 2 < total) {
+    if (c == 0 && g > 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous epilogue's stores
+    } else if (g + S - 2 < total) {
       asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * Cfg::PER_WAVE) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
