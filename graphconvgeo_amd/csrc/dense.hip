@@ -785,187 +785,6 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 #undef GCG_EPI_BV_READY
 }
 
-// Persistent form of gemm_nt_kernel (round 4, KC = 16): OCC x 256 workgroups, each walking a
-// strided share of one XCD's contiguous tile range (XCD x = b % 8 owns tiles [T x / 8, T (x+1) / 8),
-// its workgroups take every (nwg / 8)-th). The DMA ring runs over a chunk counter that spans the
-// workgroup's tiles, so the first S - 1 chunks of tile i+1 are in flight while tile i's last
-// chunks compute and its epilogue stores -- a fresh workgroup per tile starts cold instead.
-// The first chunk of every tile after the first waits vmcnt(0) (the epilogue's stores share
-// the counter with the DMA). Same per-tile arithmetic and order as gemm_nt_kernel: bitwise equal.
-template <int RT, int G, int WR, int WC, int S>
-__global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S, 16>::OCC)) void
-gemm_nt_pers_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
-                    const float* __restrict__ Bt, int64_t ldb, const float* __restrict__ bias,
-                    int act, float* __restrict__ Cout, int64_t ldc, int n_col_tiles, int n_tiles) {
-  constexpr int KC = 16;
-  using Cfg = NtCfg<RT, G, WR, WC, S, KC>;
-  constexpr int EPI = 0;
-  const int32_t* labels = nullptr;
-  float scale = 0.f;
-  const float* scale_dev = nullptr;
-  float* loss_rows = nullptr;
-  float* correct_rows = nullptr;
-  const float* row_w = nullptr;
-  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows; (void)row_w;
-  constexpr int BM = Cfg::BM, BN = Cfg::BN, STAGE = Cfg::STAGE;
-  constexpr int SL = Cfg::SL, RPI = Cfg::RPI;
-  // the DMA ring, then two bias slots of BN floats (tile parity): the bias reaches LDS by a
-  // range-checked buffer DMA issued with each tile's first chunk, so no ordinary global load
-  // (whose use would make hipcc drain the ring with vmcnt(0)) sits in the loop
-  __shared__ __attribute__((aligned(16))) float smem[Cfg::FLOATS + 2 * BN];
-  float* const sbias = smem + Cfg::FLOATS;
-  float (*red)[WC][BM] = nullptr;
-  (void)red;
-
-  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
-  const int xcd = b % 8, li = b / 8, nl = nwg / 8;  // host: nwg % 8 == 0
-  const int t_lo = static_cast<int>(static_cast<int64_t>(n_tiles) * xcd / 8);
-  const int t_hi = static_cast<int>(static_cast<int64_t>(n_tiles) * (xcd + 1) / 8);
-  const int my_tiles = li < t_hi - t_lo ? (t_hi - t_lo - li + nl - 1) / nl : 0;
-  const int n_chunks = (K + KC - 1) / KC;
-  const int total = my_tiles * n_chunks;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wave / WC, wc = wave % WC;
-  const int j = lane & 15, q = lane >> 4;
-
-  constexpr int NU = (Cfg::NGLDS + Cfg::NW - 1) / Cfg::NW;
-  int img_row[NU], kofs[NU];
-#pragma unroll
-  for (int u = 0; u < NU; ++u) {
-    const int i = wave + Cfg::NW * u;
-    img_row[u] = RPI * i + lane / SL;
-    kofs[u] = 4 * ((lane % SL) ^ nt_key<SL>(img_row[u]));
-  }
-  const int kmax4 = (K - 1) & ~3;
-  auto tile_of = [&](int i) { return t_lo + li + i * nl; };
-  auto issue = [&](int g) {
-    const int i = g / n_chunks, c = g - i * n_chunks;
-    const int tile = tile_of(i);
-    const int rt_ = tile / n_col_tiles, ct_ = tile - rt_ * n_col_tiles;
-    const int64_t r0 = static_cast<int64_t>(rt_) * BM;
-    const int c0 = ct_ * BN;
-    float* stage = smem + (g % S) * STAGE;
-#pragma unroll
-    for (int u = 0; u < NU; ++u) {
-      const int ii = wave + Cfg::NW * u;
-      if (NU * Cfg::NW != Cfg::NGLDS && ii >= Cfg::NGLDS) break;  // wave-uniform
-      const int r = img_row[u];
-      const float* src;
-      if (r < BM) {
-        const int64_t gr = r0 + r;
-        src = A + (gr < M ? gr : static_cast<int64_t>(M) - 1) * lda;
-      } else {
-        const int rb = r - BM;
-        const int n = c0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
-        src = Bt + static_cast<int64_t>(n < N ? n : N - 1) * ldb;
-      }
-      int k = c * KC + kofs[u];
-      k = k < kmax4 ? k : kmax4;
-      glds16(src + k, stage + ii * 256);
-    }
-    if (c == 0 && bias != nullptr && wave == 0) {  // lane l: bias[c0 + l] (0 past N)
-      const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(bias), static_cast<short>(0),
-                                                        N * 4, 0x00020000);
-#pragma unroll
-      for (int h = 0; h < BN / 64; ++h)
-        __builtin_amdgcn_raw_ptr_buffer_load_lds(
-            rs, (__attribute__((address_space(3))) void*)(sbias + (i & 1) * BN + 64 * h), 4,
-            (c0 + 64 * h + lane) * 4, 0, 0, 0);
-    }
-  };
-
-  f4 acc[RT][G][4];
-#pragma unroll
-  for (int t = 0; t < RT; ++t)
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
-
-  const int arow0 = wr * 16 * RT + j;
-  const int brow0 = BM + wc * G * 64 + j;
-  auto frag = [&](const float* stage, int row, int slot) -> f4 {
-    return *reinterpret_cast<const f4*>(stage + row * KC + 4 * (slot ^ nt_key<SL>(row)));
-  };
-  auto mfma_step = [&](const f4 (&af)[RT], const f4 (&bf)[G][4]) {
-#pragma unroll
-    for (int ss = 0; ss < 4; ++ss)
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int t = 0; t < RT; ++t)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[t][g][e] = mfma4(af[t][ss], bf[g][e][ss], acc[t][g][e]);
-  };
-  auto mask_step = [&](f4 (&af)[RT], f4 (&bf)[G][4], int kb) {
-    const int lim = K - kb - 4 * q;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const bool in = e < lim;
-#pragma unroll
-      for (int t = 0; t < RT; ++t) af[t][e] = in ? af[t][e] : 0.f;
-#pragma unroll
-      for (int g = 0; g < G; ++g)
-#pragma unroll
-        for (int e2 = 0; e2 < 4; ++e2) bf[g][e2][e] = in ? bf[g][e2][e] : 0.f;
-    }
-  };
-
-#pragma unroll
-  for (int g = 0; g < S - 1; ++g)
-    if (g < total) issue(g);
-  for (int g = 0; g < total; ++g) {
-    const int i = g / n_chunks, c = g - i * n_chunks;
-    if (c == 0 && g > 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // the previous epilogue's stores
-    } else if (g + S - 2 < total) {
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * Cfg::PER_WAVE) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    const float* stage = smem + (g % S) * STAGE;
-    if (g + S - 1 < total) issue(g + S - 1);
-    const int kc0 = c * KC;
-    {
-      f4 af[RT], bf[G][4];
-#pragma unroll
-      for (int t = 0; t < RT; ++t) af[t] = frag(stage, arow0 + 16 * t, q);
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) bf[gg][e] = frag(stage, brow0 + 64 * gg + 16 * e, q);
-      if (kc0 + 16 > K) mask_step(af, bf, kc0);
-      mfma_step(af, bf);
-    }
-    if (c == n_chunks - 1) {  // tile i done: epilogue, then a fresh accumulator
-      const int tile = tile_of(i);
-      const int rt_ = tile / n_col_tiles, ct_ = tile - rt_ * n_col_tiles;
-      const int64_t row0 = static_cast<int64_t>(rt_) * BM;
-      const int colw = ct_ * BN + wc * G * 64;
-      f4 bv[G];
-#pragma unroll
-      for (int gg = 0; gg < G; ++gg)
-        bv[gg] = bias != nullptr
-                     ? *reinterpret_cast<const f4*>(sbias + (i & 1) * BN + wc * G * 64 + 64 * gg + 4 * j)
-                     : f4{0.f, 0.f, 0.f, 0.f};
-#define GCG_EPI_BV_READY
-#include "gemm_epilogue.inc"
-#undef GCG_EPI_BV_READY
-#pragma unroll
-      for (int t = 0; t < RT; ++t)
-#pragma unroll
-        for (int gg = 0; gg < G; ++gg)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) acc[t][gg][e] = f4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-}
-
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
 // exp, label logit and first-index argmax, then dlogits / probabilities. In-place safe.
 template <int NV>
@@ -1532,34 +1351,7 @@ gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
   return GCG_OK;
 }
 
-// Persistent NT launch (round 4): OCC workgroups per CU over the 256 CUs (a multiple of 8:
-// the kernel splits the tiles by XCD), fewer when there are fewer tiles. Needs >= S chunks
-// per tile (the bias slots alternate by tile parity). GCG_NT_PERSIST = 0 disables it (A/B).
-template <int RT, int G, int WR, int WC, int S>
-bool launch_nt_pers(const NtArgs& a, hipStream_t st, gcg_status* status) {
-  using Cfg = NtCfg<RT, G, WR, WC, S, 16>;
-  const char* e = std::getenv("GCG_NT_PERSIST");
-  if (e != nullptr && std::atoi(e) == 0) return false;
-  if ((a.K + 15) / 16 < S) return false;
-  constexpr int BM = Cfg::BM, BN = Cfg::BN;
-  const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
-  const int64_t tiles = rt * ct;
-  if (tiles > 0x7fffffffLL) return false;
-  int64_t nwg = std::min<int64_t>(int64_t{Cfg::OCC} * 256, (tiles + 7) / 8 * 8);
-  if (const char* w = std::getenv("GCG_NT_PERSIST_WG")) nwg = std::max(8, std::atoi(w) / 8 * 8);
-  hipLaunchKernelGGL((gemm_nt_pers_kernel<RT, G, WR, WC, S>), dim3(static_cast<unsigned>(nwg)),
-                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, a.Bt, a.ldb, a.bias,
-                     a.act, a.C, a.ldc, static_cast<int>(ct), static_cast<int>(tiles));
-  const hipError_t err = hipGetLastError();
-  *status = err == hipSuccess ? GCG_OK : fail(GCG_ERR_HIP, "gemm_nt_pers: %s", hipGetErrorString(err));
-  return true;
-}
-
 gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
-  if (sh.KC == 16 && sh.RT == 2 && sh.G == 1 && sh.WR == 4 && sh.WC == 1 && sh.S == 4) {
-    gcg_status ps = GCG_OK;
-    if (launch_nt_pers<2, 1, 4, 1, 4>(a, st, &ps)) return ps;
-  }
 #define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                  \
   if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_ && \
       sh.KC == 32)                                                                               \

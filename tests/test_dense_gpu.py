@@ -322,26 +322,6 @@ def test_gemm_nt_vs_float64(cuda, M, K, N):
     _check_gemm(C, A, B)
 
 
-@pytest.mark.parametrize("M,K,N", [(1000, 300, 930), (257, 64, 65), (3000, 301, 256),
-                                   (129, 930, 300), (70, 65, 1024)])
-@pytest.mark.parametrize("wgs", ["0", "8", "24"])
-def test_gemm_nt_persistent_bitwise(cuda, M, K, N, wgs, monkeypatch):
-    """The persistent NT kernel (a DMA ring spanning each workgroup's tiles, bias by buffer DMA
-    into LDS) is bitwise the one-workgroup-per-tile kernel: with bias + rectify, ragged M / N,
-    the K tail, and 8 / 24 workgroups forcing many tiles per workgroup (0 = the default grid)."""
-    A, B, b = _rand((M, K), 41), _rand((K, N), 42), _rand((N,), 43)
-    At, bt = torch.from_numpy(A).to(cuda), torch.from_numpy(b).to(cuda)
-    Bt = _padded(B, cuda, transpose=True)
-    outs = []
-    for pers in ("0", "1"):
-        monkeypatch.setenv("GCG_NT_PERSIST", pers)
-        if wgs != "0":
-            monkeypatch.setenv("GCG_NT_PERSIST_WG", wgs)
-        outs.append((dense.gemm_nt(At, Bt, bias=bt, act="relu"), dense.gemm_nt(At, Bt)))
-    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
-    _check_gemm(outs[1][1].cpu().numpy(), A, B)
-
-
 @pytest.mark.parametrize("cfg", ["2,1,4,1,2,0", "2,1,4,1,2,1", "2,1,4,1,3,0", "2,1,4,1,3,1",
                                  "1,1,4,1,2,0", "1,1,4,1,3,0", "3,1,4,1,2,0", "2,2,4,1,2,0",
                                  "2,1,2,2,2,0", "4,1,4,1,2,0", "2,1,4,1,2,0,16",
