@@ -557,6 +557,9 @@ class TargetRowsBackward:
             g = ops.scatter_rows(n_d, self.to_distinct, g)
         out = ops.empty(part.n_local, K, part.device)
         if part.world == 1:
+            if n_d == 0:  # an empty target list: no gradient flows into Z
+                out.zero_()
+                return out
             spmm_into_ops(ops, self.A, g, out, **kw)
             return out
         c = part._n_chunks(n_chunks, K)
