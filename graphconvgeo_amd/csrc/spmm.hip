@@ -85,27 +85,6 @@ __device__ __forceinline__ Vec<VEC> load_vec_nt(const float* __restrict__ p) {
   return r;
 }
 
-// Gather with an explicit cache policy (round 4 experiment, three-tier gather hint): a buffer
-// load whose descriptor is the wave-uniform row base, the lane's column as the byte offset.
-// POL: the load's cache-policy bits (gfx950: sc0 = 1, nt = 2, sc1 = 16).
-template <int VEC, int POL>
-__device__ __forceinline__ Vec<VEC> load_vec_pol(const float* __restrict__ zrow, int col) {
-  static_assert(VEC == 4, "dwordx4 gathers only");
-  const auto rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(zrow), static_cast<short>(0),
-                                                    0x7fffffff, 0x00020000);
-  typedef float f4v __attribute__((ext_vector_type(4)));
-  const f4v t = __builtin_bit_cast(f4v, __builtin_amdgcn_raw_buffer_load_b128(rs, col * 4, 0, POL));
-  Vec<VEC> r;
-  r.x[0] = t[0]; r.x[1] = t[1]; r.x[2] = t[2]; r.x[3] = t[3];
-  return r;
-}
-
-// Hint encodings: HC = 1: bit 31 = cold column (non-temporal gather), else default policy.
-// HC >= 2 (experiment): bit 31 cold, bit 30 warm (gathered with policy kWarmPol[HC - 2]),
-// neither = hot (default policy). Column ids stay below 2^30 (host check).
-constexpr int kWarmPol[4] = {0, 1, 16, 17};
-constexpr int kHintMask = 0x3fffffff;
-
 // Non-temporal (streaming) store: Y is written once and not re-read by this kernel, so it
 // need not displace the gathered operand's hot rows from the caches (experiment knob
 // GCG_SPMM_NT_STORE=1).
@@ -238,19 +217,7 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
     Vec<VEC> z[U][NCH];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (HC >= 2) {  // three tiers: cold (nt) / warm (policy) / hot (default)
-        const float* zrow = Z + static_cast<int64_t>(c[u] & kHintMask) * ldz;
-        if (c[u] < 0) {
-#pragma unroll
-          for (int k = 0; k < NCH; ++k) z[u][k] = load_vec_nt<VEC>(zrow + col[k]);
-        } else if (c[u] & 0x40000000) {
-#pragma unroll
-          for (int k = 0; k < NCH; ++k) z[u][k] = load_vec_pol<VEC, kWarmPol[HC - 2]>(zrow, col[k]);
-        } else {
-#pragma unroll
-          for (int k = 0; k < NCH; ++k) z[u][k] = load_vec<VEC>(zrow + col[k]);
-        }
-      } else if constexpr (HC) {  // sign bit = cold column -> non-temporal gather
+      if constexpr (HC) {  // experiment: sign bit = cold column -> non-temporal gather
         const float* zrow = Z + static_cast<int64_t>(c[u] & 0x7fffffff) * ldz;
         if (c[u] < 0) {
 #pragma unroll
@@ -297,8 +264,7 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
 #pragma unroll
     for (int u = 0; u < U - 1; ++u)
       if (u < rem) {
-        const float* zrow =
-            Z + static_cast<int64_t>(HC >= 2 ? (c[u] & kHintMask) : HC ? (c[u] & 0x7fffffff) : c[u]) * ldz;
+        const float* zrow = Z + static_cast<int64_t>(HC ? (c[u] & 0x7fffffff) : c[u]) * ldz;
 #pragma unroll
         for (int k = 0; k < NCH; ++k)
           z[u][k] = load_vec<VEC>(zrow + col[k]);
@@ -421,8 +387,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c[u] = __builtin_amdgcn_readlane(ci, u);
-      if constexpr (HC >= 2) c[u] &= kHintMask;  // strip the hint bits
-      else if constexpr (HC) c[u] &= 0x7fffffff;
+      if constexpr (HC) c[u] &= 0x7fffffff;  // experiment: strip the cold-column bit
       v[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vi), u));
     }
 #pragma unroll
@@ -780,16 +745,6 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     if (a.hint != nullptr && !env_int("GCG_SPMM_NO_HINT")) {
       LaunchArgs h = a;
       h.indices = a.hint;
-      // experiment: a three-tier hint (bit 30 = warm) and the warm tier's load policy
-      // GCG_SPMM_HINT_TIERS = 3, GCG_SPMM_WARM_POL = 0 / 1 / 16 / 17 (default / sc0 / sc1 / both)
-      if (env_int("GCG_SPMM_HINT_TIERS") == 3) {
-        switch (env_int("GCG_SPMM_WARM_POL")) {
-          case 1: return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 3>(h, n_panels, stream);
-          case 16: return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 4>(h, n_panels, stream);
-          case 17: return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 5>(h, n_panels, stream);
-          default: return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 2>(h, n_panels, stream);
-        }
-      }
       return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 1>(h, n_panels, stream);
     }
     if (inflight != 64 && a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);

@@ -86,12 +86,6 @@ GATHER_HINT_HOT_BYTES = 32 << 20
 GATHER_HINT_MIN_REUSE = 4.0
 GATHER_HINT_MIN_SHARE = 0.25
 GATHER_HINT_MIN_TABLE = 256 << 20  # the Infinity Cache (US K = 256, 460 MB: 1.314 -> 1.266 ms)
-# Experiment (GCG_SPMM_HINT_TIERS=3 in the environment, read by both sides): a third, "warm"
-# tier -- the next most-gathered columns, up to GATHER_HINT_WARM_BYTES of rows and gathered at
-# least GATHER_HINT_WARM_REUSE x the mean -- marked with bit 30 and gathered with the load policy
-# GCG_SPMM_WARM_POL (spmm.hip kWarmPol). Not on by default (profiles/r04/hint_tiers.jsonl).
-GATHER_HINT_WARM_BYTES = 192 << 20
-GATHER_HINT_WARM_REUSE = 1.5
 
 
 # Integer ids of operators and row lists, for the registered torch ops (graphconvgeo_amd.ops):
@@ -366,40 +360,25 @@ class DeviceCSR:
         n_cap = max(1, GATHER_HINT_HOT_BYTES // max(1, row_bytes))
         if n_cap >= self.n_cols or self.n_cols * row_bytes < GATHER_HINT_MIN_TABLE:
             return None
-        tiers = 3 if os.environ.get("GCG_SPMM_HINT_TIERS", "") == "3" else 2
-        if tiers == 3 and self.n_cols >= 2 ** 30:
-            raise ValueError("three-tier gather hint needs column ids below 2^30")
         cache = self.__dict__.setdefault("_gather_hints", {})
-        key = (n_cap, tiers)
-        if key not in cache:
+        if n_cap not in cache:
             if torch.cuda.is_current_stream_capturing():
                 return None
             idx = self.indices.to(torch.int64)
             counts = torch.bincount(idx, minlength=self.n_cols)
-            n_top = n_cap
-            if tiers == 3:
-                n_top = min(self.n_cols, n_cap + max(1, GATHER_HINT_WARM_BYTES // max(1, row_bytes)))
-            vals, top = torch.topk(counts, n_top, sorted=True)
-            mean = self.nnz / self.n_cols
-            n_hot = int((vals[:n_cap] >= GATHER_HINT_MIN_REUSE * mean).sum())
+            vals, top = torch.topk(counts, n_cap, sorted=True)
+            thr = GATHER_HINT_MIN_REUSE * self.nnz / self.n_cols
+            n_hot = int((vals >= thr).sum())
             hint = None
             if n_hot and float(vals[:n_hot].sum()) >= GATHER_HINT_MIN_SHARE * self.nnz:
-                tier = torch.zeros(self.n_cols, dtype=torch.int8, device=self.device)  # 0 = cold
-                tier[top[:n_hot]] = 2
-                if tiers == 3:
-                    n_warm = int((vals[n_hot:] >= GATHER_HINT_WARM_REUSE * mean).sum())
-                    tier[top[n_hot:n_hot + n_warm]] = 1
-                    self._hint_warm_rows = n_warm
-                t = tier[idx]
+                hot = torch.zeros(self.n_cols, dtype=torch.bool, device=self.device)
+                hot[top[:n_hot]] = True
                 cold_bit = torch.tensor(-2 ** 31, dtype=torch.int32, device=self.device)
-                warm_bit = torch.tensor(1 << 30, dtype=torch.int32, device=self.device)
-                hint = torch.where(t == 2, self.indices,
-                                   torch.where(t == 1, self.indices | warm_bit, self.indices | cold_bit))
-                del t, tier
+                hint = torch.where(hot[idx], self.indices, self.indices | cold_bit)
             del idx, counts
             self._hint_hot_rows = n_hot
-            cache[key] = hint
-        return cache[key]
+            cache[n_cap] = hint
+        return cache[n_cap]
 
     def _dense_column_split(self):
         """The columns dense enough that A^T . G is cheaper as a dense MFMA product.

@@ -224,31 +224,6 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
         assert np.array_equal(outs["0"][2], O.spmm_f32(H, Z, rows=rows))
 
 
-@pytest.mark.parametrize("pol", [0, 1, 16, 17])
-def test_gather_hint_three_tiers_policy_only(cuda, pol, monkeypatch):
-    """Experiment: the three-tier hint (bit 30 = warm column, gathered with the load policy
-    GCG_SPMM_WARM_POL) strips to the column ids and leaves the result bitwise unchanged."""
-    monkeypatch.setattr(gs, "GATHER_HINT", True)
-    monkeypatch.setattr(gs, "GATHER_HINT_MIN_TABLE", 0)
-    monkeypatch.setattr(gs, "GATHER_HINT_HOT_BYTES", 2 << 20)
-    monkeypatch.setattr(gs, "GATHER_HINT_WARM_BYTES", 4 << 20)
-    H = synthetic_graph(20_000, 200_000)
-    Z = dense(20_000, 300)
-    A = gs.DeviceCSR.from_scipy(H, cuda, symmetric=True)
-    Zd = gs.empty_dense(20_000, 300, cuda).copy_(to_dev(Z, cuda))
-    monkeypatch.setenv("GCG_SPMM_NO_HINT", "1")
-    ref = gs.spmm(A, Zd, mode="ordered", task_nnz=256).cpu().numpy()
-    monkeypatch.delenv("GCG_SPMM_NO_HINT")
-    monkeypatch.setenv("GCG_SPMM_HINT_TIERS", "3")
-    monkeypatch.setenv("GCG_SPMM_WARM_POL", str(pol))
-    hint = A.gather_hint(1216)
-    warm = (hint >= 0) & ((hint & (1 << 30)) != 0)
-    assert hint is not None and int(warm.sum()) > 0 and int((hint < 0).sum()) > 0
-    assert torch.equal(hint & 0x3FFFFFFF, A.indices)
-    Y = gs.spmm(A, Zd, mode="ordered", task_nnz=256).cpu().numpy()
-    assert np.array_equal(Y, ref) and np.array_equal(Y, O.spmm_f32(H, Z))
-
-
 def test_gather_hint_first_call_inside_capture(cuda, monkeypatch):
     """A hint first needed inside a HIP-graph capture cannot be built there (its build syncs):
     the captured launch runs without it (default cache policy, same result) and nothing is
@@ -264,7 +239,7 @@ def test_gather_hint_first_call_inside_capture(cuda, monkeypatch):
     g = torch.cuda.CUDAGraph()
     with torch.cuda.graph(g):
         gs.spmm(A, Z, out=out, mode="ordered")
-    assert not A.__dict__.get("_gather_hints")  # not built in the capture
+    assert 4 * 2**20 // 1216 not in A.__dict__.get("_gather_hints", {})  # not built in the capture
     g.replay()
     torch.cuda.synchronize()
     eager = gs.spmm(A, Z, mode="ordered")  # builds and uses the hint

@@ -3,7 +3,8 @@
 tier (sparse.GATHER_HINT_WARM_*, bit 30) with the load policy GCG_SPMM_WARM_POL, the rest
 non-temporal -- against no hint and the two-tier hint. H.Z at K = 300 on the Twitter-World
 (power-law, uniform) and Twitter-US graphs in the mode auto resolves to, interleaved rounds,
-outputs compared bitwise. HIP events, mean of 10 launches."""
+outputs compared bitwise. HIP events, mean of 10 launches. The knobs it drives were reverted
+after the A/B (profiles/r04/hint_tiers.jsonl: slower under every policy); they live in commit 1259152."""
 import json
 import os
 import sys

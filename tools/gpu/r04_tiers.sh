@@ -1,6 +1,6 @@
 #!/bin/bash
 # Round 4 experiment: three-tier gather hint (warm tier with an explicit load policy) -- parity
-# tests, then the A/B on World power-law / US / World uniform.
+# tests, then the A/B on World power-law / US / World uniform. Needs commit 1259152 (knobs reverted).
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
