@@ -149,7 +149,7 @@ class _CSRMatMul(torch.autograd.Function):
                 # (A[rows])^T . g: one SpMM over the targets' nonzeros (sparse.rows_transpose),
                 # equal to A^T . inc_subtensor(zeros, rows, g) (mlpconv.py:94, Theano's grad)
                 # within fp32 rounding
-                # (a row-padded g -- C = 930 columns in 932-float rows -- is passed as is:
+                # (a row-padded g -- C = 930 columns in 960-float rows -- is passed as is:
                 # .contiguous() would copy it and lose the padding the 16-B gathers use)
                 g_Z = gs.spmm(A.rows_transpose(rows), g if g.stride(-1) == 1 else g.contiguous(),
                               mode=ctx.mode)

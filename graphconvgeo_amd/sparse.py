@@ -490,6 +490,9 @@ def _gathers_vec4(Z, ldz: int, Y, ldy: int, K: int, bias) -> bool:
     return K % 4 == 0 or os.environ.get("GCG_SPMM_NO_TAIL", "0") in ("", "0")
 
 
+WIDE_ROW_ALIGN = True  # row_stride: 256-B aligned rows above 512 floats (False: round-3 rule, A/B)
+
+
 def row_stride(k: int) -> int:
     """Row stride (floats) of empty_dense's k-column rows: a multiple of 4 (16-B aligned rows,
     dwordx4 loads / stores whatever k is), and among those the smallest whose row starts keep a
@@ -503,8 +506,20 @@ def row_stride(k: int) -> int:
     1500, the reference's default and tuned hidden sizes, tensormain.py:82,398), the next
     multiple of 128 B puts every row on the minimal line count instead (round 3,
     tools/exp_ld_k.py, World power-law / uniform): K = 500 at 512 floats 11.74 -> 10.99 /
-    16.14 -> 14.77 ms, K = 1500 at 1504 33.39 -> 31.89 / 44.18 -> 42.11 ms."""
+    16.14 -> 14.77 ms, K = 1500 at 1504 33.39 -> 31.89 / 44.18 -> 42.11 ms.
+    Rows wider than one 512-float column panel (round 4): the next multiple of 256 B when that
+    pads at most 1/12 of the row -- every gathered row then starts on a 256-B boundary, which a
+    random gather rewards beyond the line count (World uniform / power-law, interleaved on one
+    box, tools/exp_ld_k.py, profiles/r04/ld_sweep.jsonl): C = 930 at 960 floats 30.3 -> 28.2 /
+    20.18 -> 20.12 ms (at 932 every row already sat on the minimal 30 lines), K = 600 at 640
+    19.87 -> 18.13 / 14.03 -> 13.99, K = 1000 at 1024 32.8 -> 30.4 / 21.5 -> 20.95, K = 1500
+    at 1536 45.2 -> 40.7 / 31.0 -> 31.4 ms. At K <= 512 the 256-B strides measured slower
+    (K = 129 at 160, 258 at 288) or box-dependent (K = 300 at 320: power-law -1.6 % / +0.9 %)."""
     k4 = (k + 3) // 4 * 4
+    if k > 512 and WIDE_ROW_ALIGN:
+        k64 = (k + 63) // 64 * 64
+        if 12 * (k64 - k) <= k:
+            return k64
     if k < 32 or (4 * k) % 128 == 0:
         return k4
     slack = 128 * (-(-4 * k // 128)) - 4 * k  # bytes a row may start into its first line

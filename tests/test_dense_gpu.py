@@ -253,7 +253,7 @@ def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, layout, monkeypatch):
 def test_gemm_tn_strided_views(cuda):
     R, M, N = 3000, 300, 930
     A, B = _rand((R, M), 43), _rand((R, N), 44)
-    Bbuf = empty_dense(R, N, cuda)  # ld 932, the layout of the fused kernel's gradient
+    Bbuf = empty_dense(R, N, cuda)  # ld 960, the layout of the fused kernel's gradient
     Bbuf.copy_(torch.from_numpy(B))
     C = dense.gemm_tn(torch.from_numpy(A).to(cuda), Bbuf).cpu().numpy()
     _check_gemm(C, A.T.copy(), B)

@@ -65,7 +65,7 @@ def test_bitwise_vs_oracle(cuda, K, mode):
 @pytest.mark.parametrize("K", [1, 3, 63, 65, 129, 301, 513, 930])
 @pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
 def test_masked_tail_vec4_bitwise(cuda, K, mode, monkeypatch):
-    """K % 4 != 0 on rows padded to a multiple of 4 floats (empty_dense; C = 930 -> 932): dwordx4
+    """K % 4 != 0 on rows padded to a multiple of 4 floats (empty_dense; C = 930 -> 960): dwordx4
     gathers with a masked last vector (spmm.hip TL = 1). Bitwise equal to the narrower gathers
     (GCG_SPMM_NO_TAIL=1) and to the oracle, with bias + rectify + gate bytes, a row subset with
     duplicates, cooperative hub rows (ordered) and split rows (fast); Y's and the gate's padding

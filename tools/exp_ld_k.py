@@ -17,6 +17,9 @@ from graphconvgeo_amd.synth import CONFIGS, synthetic_graph  # noqa: E402
 dev = torch.device("cuda:0")
 cfg = CONFIGS["twitter-world"]
 cases = {300: [300, 304, 320], 500: [500, 504, 512, 528], 1500: [1500, 1504, 1536]}
+if os.environ.get("LD_CASES"):  # e.g. "930:932,936,944,960;928:928"
+    cases = {int(k): [int(x) for x in v.split(",")]
+             for k, v in (c.split(":") for c in os.environ["LD_CASES"].split(";"))}
 for kind in (sys.argv[1] if len(sys.argv) > 1 else "powerlaw,uniform").split(","):
     H = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind=kind)
     A = gs.DeviceCSR.from_scipy(H, dev, symmetric=True)
