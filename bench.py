@@ -36,6 +36,7 @@ from graphconvgeo_amd.synth import CONFIGS, SEED, synthetic_graph  # noqa: E402
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 HBM_ACHIEVABLE_GBS = 6300.0  # MI355X_MICROARCH.md:296, "~6.3 TB/s achievable"
 MFMA_F32_PEAK_TFLOPS = 157.3  # dense f32 MFMA (v_mfma_f32_16x16x4_f32) at 2.4 GHz
+MFMA_BF16_PEAK_TFLOPS = 2500.0  # dense bf16 MFMA (MI355X_MICROARCH.md; no sparsity)
 
 
 def spmm_bytes(n_rows: int, nnz: int, K: int) -> int:
@@ -364,14 +365,23 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     loss = torch.empty(T, device=dev)
     hits = torch.empty(T, device=dev)
     kernels = {
-        "gemm_nt: P.W2 + b2 (mlpconv.py:88)": lambda: dense.gemm_nt(P, W_ck, bias=b, out=G),
-        "gemm_nt: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP),
+        "gemm_nt: P.W2 + b2 (mlpconv.py:88)":
+            lambda: dense.gemm_nt(P, W_ck, bias=b, out=G, math="bf16x6"),
+        "gemm_nt: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP, math="bf16x6"),
+        "gemm_nt f32 MFMA: P.W2 + b2": lambda: dense.gemm_nt(P, W_ck, bias=b, out=G, math="f32"),
+        "gemm_nt f32 MFMA: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP, math="f32"),
         "gemm_tn: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G),
         "fused: P.W2 + b2 -> softmax-CE, hits, dlogits (mlpconv.py:88-95)":
             lambda: dense._fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits),
     }
     flops = 2.0 * T * K * C
-    out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS}
+    out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,
+           "bf16_peak_TFLOPs": MFMA_BF16_PEAK_TFLOPS,
+           "note": "TFLOPs = useful f32 FLOP/s; frac against the f32 MFMA peak. gemm_nt (the "
+                   "default, dense.NT_MATH) runs bf16x6: six bf16 plane products per f32 "
+                   "product on the bf16 matrix cores (error vs float64 <= the f32 kernel's, "
+                   "tests/test_dense_gpu.py); its frac = 6 x FLOP/s / the bf16 peak, "
+                   "f32_equivalent_frac = FLOP/s / the f32 MFMA peak"}
     for name, fn in kernels.items():
         for _ in range(5):  # the first launches after a switch run while the clock ramps
             fn()
@@ -379,6 +389,9 @@ def dense_kernels_bench(reps: int, dev) -> dict:
         tf = flops / (ms * 1e-3) / 1e12
         out[name] = {"ms": round(ms, 3), "TFLOPs": round(tf, 1),
                      "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 3)}
+        if name.startswith("gemm_nt:"):  # its roofline is the bf16 pipe: 6 MFMA FLOP per FLOP
+            out[name].update(math="bf16x6", frac=round(6 * tf / MFMA_BF16_PEAK_TFLOPS, 3),
+                             f32_equivalent_frac=round(tf / MFMA_F32_PEAK_TFLOPS, 3))
     del P, G, dP, W_kc, W_ck
     return out
 

@@ -45,6 +45,44 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
 }
 
+// f32 products on the bf16 matrix cores ("bf16x6", MX = 1 below): x = x0 + x1 + x2 with each
+// plane the round-to-nearest bf16 of what the planes before it left (8 significant bits each,
+// |x1| <= 2^-9 |x|, |x2| <= 2^-17 |x|, x - (x0 + x1 + x2) <= 2^-26 |x|). a . b keeps the six
+// plane products of order <= 2^-16 -- a0b0, a0b1, a1b0, a0b2, a1b1, a2b0 -- each exact in the
+// f32 accumulator; the dropped a1b2 + a2b1 + a2b2 are <= 2^-25 |a||b|, below f32 rounding. NaN
+// propagates (through plane 0 and the NaN residuals); an infinite operand gives NaN, not +-Inf.
+using f8 = __attribute__((ext_vector_type(8))) float;
+using bf8 = __attribute__((ext_vector_type(8))) __bf16;
+
+using f2 = __attribute__((ext_vector_type(2))) float;
+using bf2 = __attribute__((ext_vector_type(2))) __bf16;
+using u4v = __attribute__((ext_vector_type(4))) unsigned;
+
+// one pair: packed bf16 (v_cvt_pk_bf16_f32) and the f32 residual x - bf16(x), unpacked from the
+// packed word by a shift / mask instead of a second conversion
+__device__ __forceinline__ unsigned split_pair(f2& x) {
+  const unsigned p = __builtin_bit_cast(unsigned, __builtin_convertvector(x, bf2));
+  const f2 h = {__builtin_bit_cast(float, p << 16), __builtin_bit_cast(float, p & 0xffff0000u)};
+  x = x - h;
+  return p;
+}
+__device__ __forceinline__ void split3(const f8 x, bf8& h0, bf8& h1, bf8& h2) {
+  u4v p0, p1, p2;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f2 r = {x[2 * i], x[2 * i + 1]};
+    p0[i] = split_pair(r);
+    p1[i] = split_pair(r);
+    p2[i] = __builtin_bit_cast(unsigned, __builtin_convertvector(r, bf2));
+  }
+  h0 = __builtin_bit_cast(bf8, p0);
+  h1 = __builtin_bit_cast(bf8, p1);
+  h2 = __builtin_bit_cast(bf8, p2);
+}
+__device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
 template <int W>
 __device__ __forceinline__ float reduce16_max(float v) {
 #pragma unroll
@@ -556,6 +594,17 @@ __global__ __launch_bounds__(256 * WC, WC == 1 ? 2 : 1) void gemm_bl_kernel(
 typedef __attribute__((address_space(1))) const void* glds_src_t;
 typedef __attribute__((address_space(3))) void* glds_dst_t;
 
+// 16 B per lane into LDS through a buffer descriptor (base + byte range; reads past the range
+// return 0), lane byte offset voff
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void* base, int bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), static_cast<short>(0), bytes,
+                                           0x00020000);
+}
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, float* lds_wave_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds_wave_base),
+                                           16, voff, 0, 0, 0);
+}
+
 __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(reinterpret_cast<glds_src_t>(reinterpret_cast<uintptr_t>(src)),
                                    (glds_dst_t)(lds_wave_base), 16, 0, 0);
@@ -592,7 +641,7 @@ __device__ __forceinline__ int nt_key(int r) {
   else return (0x78 >> (2 * ((r >> 2) & 3))) & 3;  // pi packed 2 bits each: 0, 2, 3, 1
 }
 
-template <int RT, int G, int WR, int WC, int S, int PF, int KC>
+template <int RT, int G, int WR, int WC, int S, int PF, int KC, int MX = 0>
 __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S, KC>::OCC)) void
 gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ Bt, int64_t ldb, const float* __restrict__ bias, int act,
@@ -756,6 +805,40 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       read_step(stage, 0, af, bf);
       if (kc0 + 16 > K) mask_step(af, bf, kc0);
       mfma_step(af, bf);
+    } else if constexpr (MX == 1) {
+      // bf16x6: the chunk's two 16-deep fragment sets are one 32-deep bf16 MFMA operand (lane
+      // (j, q) holds k = kc0 + 4q + {0..3} and kc0 + 16 + 4q + {0..3}, the same for A and B)
+      f4 af0[RT], bf0[G][4], af1[RT], bf1[G][4];
+      read_step(stage, 0, af0, bf0);
+      read_step(stage, 1, af1, bf1);
+      if (kc0 + 16 > K) mask_step(af0, bf0, kc0);
+      if (kc0 + 32 > K) mask_step(af1, bf1, kc0 + 16);
+      bf8 ap[RT][3];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const f8 x = {af0[t][0], af0[t][1], af0[t][2], af0[t][3],
+                      af1[t][0], af1[t][1], af1[t][2], af1[t][3]};
+        split3(x, ap[t][0], ap[t][1], ap[t][2]);
+      }
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f8 y = {bf0[g][e][0], bf0[g][e][1], bf0[g][e][2], bf0[g][e][3],
+                        bf1[g][e][0], bf1[g][e][1], bf1[g][e][2], bf1[g][e][3]};
+          bf8 b0, b1, b2;
+          split3(y, b0, b1, b2);
+#pragma unroll
+          for (int t = 0; t < RT; ++t) {  // smallest planes first
+            f4 c = acc[t][g][e];
+            c = mfma_bf(ap[t][2], b0, c);
+            c = mfma_bf(ap[t][1], b1, c);
+            c = mfma_bf(ap[t][0], b2, c);
+            c = mfma_bf(ap[t][1], b0, c);
+            c = mfma_bf(ap[t][0], b1, c);
+            acc[t][g][e] = mfma_bf(ap[t][0], b0, c);
+          }
+        }
     } else if constexpr (PF) {
       // both 16-deep steps' fragments first: the second step's LDS reads are in flight
       // during the first step's MFMAs (counted lgkmcnt waits)
@@ -779,6 +862,408 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
         mfma_step(af, bf);
       }
     }
+  }
+#define GCG_EPI_BV_READY
+#include "gemm_epilogue.inc"
+#undef GCG_EPI_BV_READY
+}
+
+// ---------------------------------------------------------------------------------------
+// bf16x6 NT GEMM with the weight side pre-split (round 4): C = act(A . Bt^T + bias) with
+// Bt's three bf16 planes written once per call by split3_rows_kernel into a workspace laid out
+// [N][Kc][3][32] bf16 (Kc = ceil(K / 32) chunks, zeros past K), each 32-element plane chunk in
+// the k order of the MFMA operand (position 8q + w holds k = 4q + w for w < 4, 16 + 4q + w - 4
+// after), so a lane's B fragment of one plane is ONE 16-B LDS read and no B conversion is left
+// in the loop. A stays f32 (staged exactly as gemm_nt_kernel's KC = 32 image) and is split in
+// registers. LDS stage: [BM rows][8 slots] f32, then per plane [BN rows][4 slots] (64-B rows,
+// swizzle nt_key<4>, the conflict-free 4-slot layout of the KC = 16 kernel), all through the
+// LDS-DMA ring. The B image keeps gemm_nt_kernel's strided row order (row 16e + j of a 64-column
+// group holds column 4j + e), so the accumulator layout and the epilogue are the same.
+// ---------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void split3_rows_kernel(int N, int K, int Kc,
+                                                          const float* __restrict__ Bt, int64_t ldb,
+                                                          unsigned* __restrict__ out) {
+  const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;  // (n, chunk, q)
+  if (i >= static_cast<int64_t>(N) * Kc * 4) return;
+  const int q = static_cast<int>(i & 3);
+  const int64_t nc = i >> 2;
+  const int n = static_cast<int>(nc / Kc), c = static_cast<int>(nc % Kc);
+  const float* row = Bt + static_cast<int64_t>(n) * ldb;
+  f8 x;
+#pragma unroll
+  for (int w = 0; w < 8; ++w) {
+    const int k = 32 * c + (w < 4 ? 4 * q + w : 16 + 4 * q + (w - 4));
+    x[w] = k < K ? row[k] : 0.f;
+  }
+  bf8 h[3];
+  split3(x, h[0], h[1], h[2]);
+  // [n][c][plane][32 bf16]: plane p's lane-q fragment is the 16 B at (nc * 3 + p) * 64 + 16 q
+#pragma unroll
+  for (int p = 0; p < 3; ++p)
+    *reinterpret_cast<u4v*>(out + (nc * 3 + p) * 16 + 4 * q) = __builtin_bit_cast(u4v, h[p]);
+}
+
+template <int RT, int G, int WR, int WC, int S>
+struct Nt3Cfg {
+  static constexpr int NW = WR * WC;
+  static constexpr int BM = 16 * RT * WR;
+  static constexpr int BN = 64 * G * WC;
+  static constexpr int A_FLOATS = BM * 32;          // [BM][8 slots of 16 B]
+  static constexpr int P_FLOATS = BN * 16;          // one plane: [BN][4 slots of 16 B]
+  static constexpr int STAGE = A_FLOATS + 3 * P_FLOATS;
+  static constexpr int NGA = BM / 8;                // DMA wave-instructions (1 KB each)
+  static constexpr int NGP = BN / 16;               // ... per plane
+  static constexpr int NG = NGA + 3 * NGP;
+  static constexpr int NU = (NG + NW - 1) / NW;
+  static constexpr int PER_WAVE = NG / NW;          // (exact when S >= 3)
+  static constexpr int FLOATS = S * STAGE;
+  static constexpr int OCC_LDS = (160 * 1024) / (FLOATS * 4);
+  static constexpr int OCC = OCC_LDS < 1 ? 1 : (OCC_LDS > 4 ? 4 : OCC_LDS);
+  static_assert(S == 2 || NG % NW == 0, "S >= 3 needs the same DMA count on every wave");
+  static_assert(S >= 2 && S <= 4, "2..4 stages");
+};
+
+template <int RT, int G, int WR, int WC, int S>
+__global__ __launch_bounds__(64 * WR * WC, (Nt3Cfg<RT, G, WR, WC, S>::OCC)) void
+gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
+                const unsigned* __restrict__ Bs, const float* __restrict__ bias, int act,
+                float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
+  using Cfg = Nt3Cfg<RT, G, WR, WC, S>;
+  constexpr int EPI = 0;
+  const int32_t* labels = nullptr;
+  float scale = 0.f;
+  const float* scale_dev = nullptr;
+  float* loss_rows = nullptr;
+  float* correct_rows = nullptr;
+  const float* row_w = nullptr;
+  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows; (void)row_w;
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, STAGE = Cfg::STAGE, NW = Cfg::NW, NU = Cfg::NU;
+  __shared__ __attribute__((aligned(16))) float smem[Cfg::FLOATS];
+  float (*red)[WC][BM] = nullptr;
+  (void)red;
+
+  const int nwg = static_cast<int>(gridDim.x);
+  const int b = static_cast<int>(blockIdx.x);
+  const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+  const int row_tile = tile / n_col_tiles, col_tile = tile % n_col_tiles;
+  const int64_t row0 = static_cast<int64_t>(row_tile) * BM;
+  const int col0 = col_tile * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int j = lane & 15, q = lane >> 4;
+  const int colw = col0 + wc * G * 64;
+  const int Kc = (K + 31) / 32;
+
+  // DMA sources, through buffer descriptors re-based every chunk (scalar work only; the lane
+  // offsets are constants): instruction i < NGA fills A image rows 8i .. 8i+7 (8 slots, key
+  // r & 7), the others plane p = (i - NGA) / NGP, plane rows 16 ib .. 16 ib + 15 (4 slots, key
+  // nt_key<4>). A's range ends at the tile's last row's round4(K): the K-tail chunk's segments
+  // past it read 0 (rows inside read their neighbours' floats, zeroed in registers below).
+  static_assert(Cfg::NGA % NW == 0, "A and B DMA instructions split at a whole u");
+  constexpr int UA = Cfg::NGA / NW;
+  int voff[NU];
+  const int rows_here = static_cast<int>(M - row0 < BM ? M - row0 : BM);
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = wave + NW * u;
+    if (u < UA) {
+      const int r = 8 * i + lane / 8;
+      const int rl = r < rows_here ? r : rows_here - 1;
+      voff[u] = (rl * static_cast<int>(lda) + 4 * ((lane % 8) ^ (r & 7))) * 4;
+    } else {
+      const int ib = i - Cfg::NGA;
+      const int p = ib / Cfg::NGP;
+      const int rb = (ib % Cfg::NGP) * 16 + lane / 4;
+      const int sl = (lane % 4) ^ nt_key<4>(rb);
+      int n = col0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
+      n = n < N ? n : N - 1;
+      voff[u] = ((n * Kc) * 3 + p) * 64 + 16 * sl;
+    }
+  }
+  const int a_bytes = ((rows_here - 1) * static_cast<int>(lda) + ((K + 3) & ~3)) * 4;
+  const int b_bytes = N * Kc * 192;
+  auto issue = [&](int chunk) {
+    float* stage = smem + (chunk % S) * STAGE;
+    const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
+    const auto rbs = brsrc(Bs + 48 * chunk, b_bytes - 192 * chunk);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = wave + NW * u;
+      if (NU * NW != Cfg::NG && i >= Cfg::NG) break;  // wave-uniform
+      blds16(u < UA ? ra : rbs, stage + i * 256, voff[u]);
+    }
+  };
+  auto lds_barrier = [&]() {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  };
+
+  f4 acc[RT][G][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bv[g] = f4{0.f, 0.f, 0.f, 0.f};
+    const int c = colw + 64 * g + 4 * j;
+    if (bias != nullptr) {
+      if (c + 3 < N) {
+        bv[g] = f4{bias[c], bias[c + 1], bias[c + 2], bias[c + 3]};
+      } else {
+        if (c < N) bv[g].x = bias[c];
+        if (c + 1 < N) bv[g].y = bias[c + 1];
+        if (c + 2 < N) bv[g].z = bias[c + 2];
+      }
+    }
+  }
+
+  const int arow0 = wr * 16 * RT + j;
+  const int brow0 = wc * G * 64 + j;
+  for (int c = 0; c < S - 1; ++c)
+    if (c < Kc) issue(c);
+  for (int c = 0; c < Kc; ++c) {
+    if constexpr (S == 2) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (c + S - 2 < Kc) {
+        asm volatile("s_waitcnt vmcnt(%0)" :: "n"((S - 2) * Cfg::PER_WAVE) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+    }
+    lds_barrier();
+    const float* stage = smem + (c % S) * STAGE;
+    const int kc0 = c * 32;
+    if (c + S - 1 < Kc) issue(c + S - 1);
+    // A fragments (two 16-B reads per tile), masked past K, split into planes
+    bf8 ap[RT][3];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const int r = arow0 + 16 * t;
+      const f4 lo = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * (q ^ (r & 7)));
+      const f4 hi = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * ((4 + q) ^ (r & 7)));
+      f8 x = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (kc0 + 32 > K) {
+        const int lim = K - kc0 - 4 * q;  // lo element w: k = kc0 + 4q + w; hi: + 16
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          x[w] = w < lim ? x[w] : 0.f;
+          x[4 + w] = 16 + w < lim ? x[4 + w] : 0.f;
+        }
+      }
+      split3(x, ap[t][0], ap[t][1], ap[t][2]);
+    }
+    const float* bsec = stage + Cfg::A_FLOATS;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rb = brow0 + 64 * g + 16 * e;
+        const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
+        const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
+        const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
+        const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {  // smallest planes first
+          f4 cc = acc[t][g][e];
+          cc = mfma_bf(ap[t][2], b0, cc);
+          cc = mfma_bf(ap[t][1], b1, cc);
+          cc = mfma_bf(ap[t][0], b2, cc);
+          cc = mfma_bf(ap[t][1], b0, cc);
+          cc = mfma_bf(ap[t][0], b1, cc);
+          acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+        }
+      }
+  }
+#define GCG_EPI_BV_READY
+#include "gemm_epilogue.inc"
+#undef GCG_EPI_BV_READY
+}
+
+// gemm_nt3r_kernel<RT, G, WR, WC>: gemm_nt3_kernel with A loaded straight into registers (each
+// wave owns its 16 RT rows, so an LDS stage of A is shared by nobody when WC = 1): two
+// dwordx4 buffer loads per row tile and chunk through a descriptor re-based every chunk, one
+// chunk ahead (two register sets, the chunk loop unrolled by two), while only the weight's
+// planes go through the LDS-DMA ring (12 KB per 64 columns and chunk, two stages), so more
+// workgroups fit per CU.
+template <int RT, int G, int WR, int WC>
+struct Nt3rCfg {
+  static constexpr int NW = WR * WC;
+  static constexpr int BM = 16 * RT * WR;
+  static constexpr int BN = 64 * G * WC;
+  static constexpr int P_FLOATS = BN * 16;
+  static constexpr int STAGE = 3 * P_FLOATS;
+  static constexpr int NGP = BN / 16;
+  static constexpr int NG = 3 * NGP;
+  static constexpr int NU = (NG + NW - 1) / NW;
+  static constexpr int FLOATS = 2 * STAGE;
+  static constexpr int OCC_LDS = (160 * 1024) / (FLOATS * 4);
+  static constexpr int OCC_REG = RT * G >= 4 ? 2 : 4;  // 4 x 4 accumulator tiles: <= 256 VGPRs
+  static constexpr int OCC = OCC_LDS < 1 ? 1 : (OCC_LDS > OCC_REG ? OCC_REG : OCC_LDS);
+};
+
+template <int RT, int G, int WR, int WC>
+__global__ __launch_bounds__(64 * WR * WC, (Nt3rCfg<RT, G, WR, WC>::OCC)) void
+gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
+                 const unsigned* __restrict__ Bs, const float* __restrict__ bias, int act,
+                 float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
+  using Cfg = Nt3rCfg<RT, G, WR, WC>;
+  constexpr int EPI = 0;
+  const int32_t* labels = nullptr;
+  float scale = 0.f;
+  const float* scale_dev = nullptr;
+  float* loss_rows = nullptr;
+  float* correct_rows = nullptr;
+  const float* row_w = nullptr;
+  (void)labels; (void)scale; (void)scale_dev; (void)loss_rows; (void)correct_rows; (void)row_w;
+  constexpr int BM = Cfg::BM, BN = Cfg::BN, STAGE = Cfg::STAGE, NW = Cfg::NW, NU = Cfg::NU;
+  __shared__ __attribute__((aligned(16))) float smem[Cfg::FLOATS];
+  float (*red)[WC][BM] = nullptr;
+  (void)red;
+
+  const int nwg = static_cast<int>(gridDim.x);
+  const int b = static_cast<int>(blockIdx.x);
+  const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+  const int row_tile = tile / n_col_tiles, col_tile = tile % n_col_tiles;
+  const int64_t row0 = static_cast<int64_t>(row_tile) * BM;
+  const int col0 = col_tile * BN;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wave / WC, wc = wave % WC;
+  const int j = lane & 15, q = lane >> 4;
+  const int colw = col0 + wc * G * 64;
+  const int Kc = (K + 31) / 32;
+  const int rows_here = static_cast<int>(M - row0 < BM ? M - row0 : BM);
+
+  // weight planes: LDS-DMA instruction i fills plane p = i / NGP, rows 16 (i % NGP) .. + 15
+  int voff[NU];
+#pragma unroll
+  for (int u = 0; u < NU; ++u) {
+    const int i = wave + NW * u;
+    const int p = i / Cfg::NGP;
+    const int rb = (i % Cfg::NGP) * 16 + lane / 4;
+    const int sl = (lane % 4) ^ nt_key<4>(rb);
+    int n = col0 + (rb & ~63) + 4 * (rb & 15) + ((rb >> 4) & 3);
+    n = n < N ? n : N - 1;
+    voff[u] = ((n * Kc) * 3 + p) * 64 + 16 * sl;
+  }
+  // A: lane (j, q) of row tile t reads row wr*16RT + 16t + j, k = 4q..4q+3 and 16+4q..16+4q+3
+  int aoff[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    int r = wr * 16 * RT + 16 * t + j;
+    r = r < rows_here ? r : rows_here - 1;
+    aoff[t] = (r * static_cast<int>(lda) + 4 * q) * 4;
+  }
+  const int a_bytes = ((rows_here - 1) * static_cast<int>(lda) + ((K + 3) & ~3)) * 4;
+  const int b_bytes = N * Kc * 192;
+  auto issue_b = [&](int chunk) {
+    float* stage = smem + (chunk & 1) * STAGE;
+    const auto rbs = brsrc(Bs + 48 * chunk, b_bytes - 192 * chunk);
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int i = wave + NW * u;
+      if (NU * NW != Cfg::NG && i >= Cfg::NG) break;  // wave-uniform
+      blds16(rbs, stage + i * 256, voff[u]);
+    }
+  };
+  auto load_a = [&](int chunk, f4 (&lo)[RT], f4 (&hi)[RT]) {
+    const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      lo[t] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff[t], 0, 0));
+      hi[t] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff[t] + 64, 0, 0));
+    }
+  };
+
+  f4 acc[RT][G][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    bv[g] = f4{0.f, 0.f, 0.f, 0.f};
+    const int c = colw + 64 * g + 4 * j;
+    if (bias != nullptr) {
+      if (c + 3 < N) {
+        bv[g] = f4{bias[c], bias[c + 1], bias[c + 2], bias[c + 3]};
+      } else {
+        if (c < N) bv[g].x = bias[c];
+        if (c + 1 < N) bv[g].y = bias[c + 1];
+        if (c + 2 < N) bv[g].z = bias[c + 2];
+      }
+    }
+  }
+
+  const int brow0 = wc * G * 64 + j;
+  auto step = [&](int c, f4 (&lo)[RT], f4 (&hi)[RT], f4 (&nlo)[RT], f4 (&nhi)[RT]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c: its A registers and B planes
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 1 < Kc) {
+      issue_b(c + 1);
+      load_a(c + 1, nlo, nhi);
+    }
+    const int kc0 = c * 32;
+    bf8 ap[RT][3];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      f8 x = {lo[t][0], lo[t][1], lo[t][2], lo[t][3], hi[t][0], hi[t][1], hi[t][2], hi[t][3]};
+      if (kc0 + 32 > K) {
+        const int lim = K - kc0 - 4 * q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          x[w] = w < lim ? x[w] : 0.f;
+          x[4 + w] = 16 + w < lim ? x[4 + w] : 0.f;
+        }
+      }
+      split3(x, ap[t][0], ap[t][1], ap[t][2]);
+    }
+    const float* bsec = smem + (c & 1) * STAGE;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int rb = brow0 + 64 * g + 16 * e;
+        const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
+        const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
+        const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
+        const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {
+          f4 cc = acc[t][g][e];
+          cc = mfma_bf(ap[t][2], b0, cc);
+          cc = mfma_bf(ap[t][1], b1, cc);
+          cc = mfma_bf(ap[t][0], b2, cc);
+          cc = mfma_bf(ap[t][1], b0, cc);
+          cc = mfma_bf(ap[t][0], b1, cc);
+          acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+        }
+      }
+  };
+  f4 alo[RT], ahi[RT], blo[RT], bhi[RT];
+  issue_b(0);
+  load_a(0, alo, ahi);
+  for (int c = 0; c < Kc; c += 2) {
+    step(c, alo, ahi, blo, bhi);
+    if (c + 1 < Kc) step(c + 1, blo, bhi, alo, ahi);
   }
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
@@ -1296,7 +1781,7 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
 // NT GEMM tile variants: (RT, G, WR, WC, S). Default BM = 256 x BN = 64, two stages,
 // two workgroups per CU (80 KB of LDS each); the others are experiment knobs (GCG_NT_CFG).
 struct NtShape {
-  int RT, G, WR, WC, S, PF = 0, KC = 32;
+  int RT, G, WR, WC, S, PF = 0, KC = 32, MX = 0;
   int bm() const { return 16 * RT * WR; }
   int bn() const { return 64 * G * WC; }
 };
@@ -1338,12 +1823,36 @@ struct NtArgs {
   int64_t ldc;
 };
 
-template <int RT, int G, int WR, int WC, int S, int PF, int KC>
+template <int RT, int G, int WR, int WC, int S>
+gcg_status launch_nt3_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
+  constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
+  const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
+  if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
+  hipLaunchKernelGGL((gemm_nt3_kernel<RT, G, WR, WC, S>), dim3(static_cast<unsigned>(rt * ct)),
+                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.bias, a.act, a.C,
+                     a.ldc, static_cast<int>(ct));
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+template <int RT, int G, int WR, int WC>
+gcg_status launch_nt3r_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
+  constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
+  const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
+  if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
+  hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC>), dim3(static_cast<unsigned>(rt * ct)),
+                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.bias, a.act, a.C,
+                     a.ldc, static_cast<int>(ct));
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
+}
+
+template <int RT, int G, int WR, int WC, int S, int PF, int KC, int MX = 0>
 gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
-  hipLaunchKernelGGL((gemm_nt_kernel<RT, G, WR, WC, S, PF, KC>),
+  hipLaunchKernelGGL((gemm_nt_kernel<RT, G, WR, WC, S, PF, KC, MX>),
                      dim3(static_cast<unsigned>(rt * ct)), dim3(64 * WR * WC), 0, st, a.M, a.N,
                      a.K, a.A, a.lda, a.Bt, a.ldb, a.bias, a.act, a.C, a.ldc,
                      static_cast<int>(ct));
@@ -1352,6 +1861,18 @@ gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
 }
 
 gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
+#define GCG_NTX_CASE(rt_, g_, wr_, wc_, s_)                                                     \
+  if (sh.MX == 1 && sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_)   \
+    return launch_nt_t<rt_, g_, wr_, wc_, s_, 1, 32, 1>(a, st);
+  GCG_NTX_CASE(2, 1, 4, 1, 2)
+  GCG_NTX_CASE(2, 1, 4, 1, 3)
+  GCG_NTX_CASE(4, 1, 4, 1, 2)
+  GCG_NTX_CASE(2, 2, 4, 1, 2)
+  GCG_NTX_CASE(2, 1, 2, 2, 2)
+#undef GCG_NTX_CASE
+  if (sh.MX != 0)
+    return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt: no bf16x6 tile RT=%d G=%d WR=%d WC=%d S=%d",
+                sh.RT, sh.G, sh.WR, sh.WC, sh.S);
 #define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                  \
   if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_ && \
       sh.KC == 32)                                                                               \
@@ -1384,6 +1905,73 @@ gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
               sh.RT, sh.G, sh.WR, sh.WC, sh.S, sh.PF, sh.KC);
 }
 
+// bf16x6 tiles (MX = 1; 32-deep chunks): default 128 x 64, two stages; GCG_NTX_CFG =
+// "RT,G,WR,WC,S" picks another (experiment knob).
+NtShape pick_ntx_shape() {
+  NtShape sh{2, 1, 4, 1, 2, 1, 32, 1};
+  if (const char* v = std::getenv("GCG_NTX_CFG")) {
+    int a = 0, b = 0, c = 0, d = 0, e = 0;
+    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) == 5) sh = NtShape{a, b, c, d, e, 1, 32, 1};
+  }
+  return sh;
+}
+
+gcg_status gemm_nt_common(const char* fn, int mx, int64_t M, int64_t N, int64_t K, const float* A,
+                          int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int act,
+                          float* C, int64_t ldc, gcg_stream_t stream);
+
+// pre-split bf16x6 tiles (gemm_nt3_kernel): default 128 x 64, two stages; GCG_NT3_CFG =
+// "RT,G,WR,WC,S" picks another (experiment knob; S = 0: gemm_nt3r_kernel, A in registers).
+struct Nt3Shape {
+  int RT, G, WR, WC, S;
+};
+// Measured (tools/exp_gemm_bf16x6.py, one box, f32-equivalent TFLOP/s; f32 MFMA kernel 113-119):
+//   shape (M x K x N)     LDS A: 2,1,4,1,2  2,2,4,1,2  2,1,4,2,2 | register A: 2,1,4,1  2,2,4,1  4,1,4,1
+//   840k x 300 x 930           146          151-156     154-155  |             164-165  170-172  151-154
+//   840k x 930 x 300           167          165-166     155      |             159-160  164      154-157
+//   1.4M x 300 x 930           146          151-152     154-155  |             165-166  171      151
+//   450k x 300 x 256           138-141      155         154-155  |             155-157  168-170  141-142
+//   450k x 256 x 300           136          138-139     134-137  |             143-145  142      129
+// (deeper rings, S = 3, lost 15-30: one workgroup per CU). Default: register A, 128 x 128.
+Nt3Shape pick_nt3_shape() {
+  Nt3Shape sh{2, 2, 4, 1, 0};
+  if (const char* v = std::getenv("GCG_NT3_CFG")) {
+    int a = 0, b = 0, c = 0, d = 0, e = 0;
+    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) == 5) sh = Nt3Shape{a, b, c, d, e};
+  }
+  return sh;
+}
+gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const unsigned* Bs) {
+#define GCG_NT3_CASE(rt_, g_, wr_, wc_, s_)                                                    \
+  if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_)                \
+    return launch_nt3_t<rt_, g_, wr_, wc_, s_>(a, Bs, st);
+  GCG_NT3_CASE(2, 1, 4, 1, 2)
+  GCG_NT3_CASE(2, 1, 4, 1, 3)
+  GCG_NT3_CASE(4, 1, 4, 1, 2)
+  GCG_NT3_CASE(2, 2, 4, 1, 2)
+  GCG_NT3_CASE(2, 2, 4, 1, 3)
+  GCG_NT3_CASE(2, 1, 2, 2, 2)
+  GCG_NT3_CASE(4, 1, 2, 2, 2)
+  GCG_NT3_CASE(2, 1, 4, 2, 2)
+  GCG_NT3_CASE(2, 1, 4, 2, 3)
+  GCG_NT3_CASE(2, 2, 4, 2, 2)
+  GCG_NT3_CASE(4, 1, 4, 2, 2)
+#undef GCG_NT3_CASE
+#define GCG_NT3R_CASE(rt_, g_, wr_, wc_)                                                       \
+  if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == 0)                 \
+    return launch_nt3r_t<rt_, g_, wr_, wc_>(a, Bs, st);
+  GCG_NT3R_CASE(2, 1, 4, 1)
+  GCG_NT3R_CASE(2, 2, 4, 1)
+  GCG_NT3R_CASE(4, 1, 4, 1)
+  GCG_NT3R_CASE(2, 1, 2, 1)
+  GCG_NT3R_CASE(2, 2, 2, 1)
+  GCG_NT3R_CASE(4, 1, 2, 1)
+  GCG_NT3R_CASE(2, 1, 4, 2)
+#undef GCG_NT3R_CASE
+  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32_bf16x6: no tile RT=%d G=%d WR=%d WC=%d S=%d",
+              sh.RT, sh.G, sh.WR, sh.WC, sh.S);
+}
+
 }  // namespace
 
 extern "C" {
@@ -1391,7 +1979,49 @@ extern "C" {
 gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                            const float* Bt, int64_t ldbt, const float* bias, int act, float* C,
                            int64_t ldc, gcg_stream_t stream) {
-  const char* fn = "gcg_gemm_nt_f32";
+  return gemm_nt_common("gcg_gemm_nt_f32", 0, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
+}
+
+int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K) {
+  if (N <= 0 || K <= 0) return 0;
+  return N * ((K + 31) / 32) * 192;
+}
+
+gcg_status gcg_gemm_nt_f32_bf16x6(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                  const float* Bt, int64_t ldbt, const float* bias, int act,
+                                  float* C, int64_t ldc, void* ws, int64_t ws_bytes,
+                                  gcg_stream_t stream) {
+  const char* fn = "gcg_gemm_nt_f32_bf16x6";
+  // no workspace, or planes / A tiles past the 32-bit buffer offsets: both operands split in
+  // the loop (gemm_nt_kernel MX = 1)
+  if (ws != nullptr && (gcg_gemm_nt_bf16x6_workspace(N, K) > INT32_MAX || 256 * lda * 4 > INT32_MAX / 2))
+    ws = nullptr;
+  if (ws == nullptr)
+    return gemm_nt_common(fn, 1, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
+  if (ws_bytes < gcg_gemm_nt_bf16x6_workspace(N, K))
+    return fail(GCG_ERR_INVALID_ARG, "%s: workspace %lld B < %lld B", fn,
+                static_cast<long long>(ws_bytes),
+                static_cast<long long>(gcg_gemm_nt_bf16x6_workspace(N, K)));
+  if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
+  gcg_status s = gemm_nt_common(fn, 2, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
+  if (s != GCG_OK || M == 0) return s;
+  const int Kc = static_cast<int>((K + 31) / 32);
+  const int64_t threads = N * Kc * 4;
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256),
+                     0, st, int(N), int(K), Kc, Bt, ldbt, static_cast<unsigned*>(ws));
+  GCG_HIP_CHECK(hipGetLastError());
+  NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
+  return launch_nt3(pick_nt3_shape(), st, a, static_cast<const unsigned*>(ws));
+}
+
+}  // extern "C"
+
+namespace {
+
+gcg_status gemm_nt_common(const char* fn, int mx, int64_t M, int64_t N, int64_t K, const float* A,
+                          int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int act,
+                          float* C, int64_t ldc, gcg_stream_t stream) {
   if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
                 static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
@@ -1404,9 +2034,14 @@ gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
   if ((s = check_dense(fn, C, ldc, N, true)) != GCG_OK) return s;
   if (bias != nullptr && !aligned(bias, 4)) return fail(GCG_ERR_MISALIGNED, "%s: bias", fn);
   if (M == 0) return GCG_OK;
+  if (mx == 2) return GCG_OK;  // validation only (the pre-split path launches itself)
   NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
-  return launch_nt(pick_nt_shape(K), static_cast<hipStream_t>(stream), a);
+  return launch_nt(mx ? pick_ntx_shape() : pick_nt_shape(K), static_cast<hipStream_t>(stream), a);
 }
+
+}  // namespace
+
+extern "C" {
 
 gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         const float* B, int64_t ldb, const float* bias, int act, float* C,

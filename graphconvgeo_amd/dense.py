@@ -30,7 +30,7 @@ import ctypes as C
 import torch
 
 from . import ops as _ops  # registers torch.ops.gcg.* (the compiled path)
-from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call
+from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call, load
 from .sparse import _ptr, _require_cuda, _stream_handle, column_sum, empty_dense
 
 FUSED_MAX_COLS = 1024
@@ -119,11 +119,26 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
     return out
 
 
+# gemm_nt's default products: "bf16x6" (round 4: f32 operands split into three bf16 planes on
+# the bf16 matrix cores, error against float64 at or below the f32 MFMA kernel's,
+# tests/test_dense_gpu.py; 164-171 vs 113-119 TFLOP/s at Twitter-World's shapes) or "f32"
+# (v_mfma_f32_16x16x4_f32).
+NT_MATH = "bf16x6"
+NT_MATHS = ("f32", "bf16x6", "bf16x6_inloop")
+
+
 def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = None,
-            act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+            act: Optional[str] = None, out: Optional[torch.Tensor] = None,
+            math: Optional[str] = None) -> torch.Tensor:
     """C = act(A . Bt^T + bias) on the LDS-DMA MFMA kernel (gcg_gemm_nt_f32): both operands
     k-contiguous, 16-B aligned rows (A: M x K, Bt: N x K). The weight side is a transposed
-    padded copy (_WeightCache(transpose=True)) for A . W, or W itself (padded) for g . W^T."""
+    padded copy (_WeightCache(transpose=True)) for A . W, or W itself (padded) for g . W^T.
+    math: "f32" (v_mfma_f32_16x16x4_f32) or "bf16x6" (gcg_gemm_nt_f32_bf16x6: f32-accurate
+    products from three bf16 planes per operand on the bf16 matrix cores, Bt's planes split
+    once into a workspace; "bf16x6_inloop" splits both operands in the loop); None: NT_MATH."""
+    math = math or NT_MATH
+    if math not in NT_MATHS:
+        raise ValueError(f"math must be one of {NT_MATHS}")
     A = _aligned_operand(A, "A")
     Bt = _aligned_operand(Bt, "Bt")
     M, K = A.shape
@@ -146,8 +161,16 @@ def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = No
         return out
     actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
     with torch.cuda.device(A.device):
-        call("gcg_gemm_nt_f32", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt), _ptr(bias), actc,
-             _ptr(out), _ld(out), _stream_handle(A.device))
+        if math == "f32":
+            call("gcg_gemm_nt_f32", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt), _ptr(bias), actc,
+                 _ptr(out), _ld(out), _stream_handle(A.device))
+        else:
+            ws, nb = None, 0
+            if math == "bf16x6":
+                nb = int(load().gcg_gemm_nt_bf16x6_workspace(N, K))
+                ws = torch.empty(nb, dtype=torch.uint8, device=A.device)  # stream-ordered
+            call("gcg_gemm_nt_f32_bf16x6", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt),
+                 _ptr(bias), actc, _ptr(out), _ld(out), _ptr(ws), nb, _stream_handle(A.device))
     return out
 
 

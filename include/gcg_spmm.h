@@ -353,6 +353,24 @@ gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int6
                            int act, float* C, int64_t ldc, gcg_stream_t stream);
 
 /*
+ * gcg_gemm_nt_f32_bf16x6: gcg_gemm_nt_f32 (same operands, layout rules and padding guarantee)
+ * with the products on the bf16 matrix cores: every f32 fragment is split in registers into
+ * three bf16 planes x = x0 + x1 + x2 (round to nearest, 8 significant bits each) and the six
+ * plane products of order <= 2^-16 are accumulated in f32 (v_mfma_f32_16x16x32_bf16), each
+ * exact. Accuracy is f32's: the dropped cross terms are <= 2^-25 |a||b| per product, below the
+ * rounding of an f32 accumulation (tests/test_dense_gpu.py compares the error against float64
+ * with the f32 kernel's). NaN propagates; an infinite operand yields NaN instead of +-Inf.
+ */
+gcg_status gcg_gemm_nt_f32_bf16x6(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                  const float* Bt, int64_t ldbt, const float* bias /*nullable*/,
+                                  int act, float* C, int64_t ldc, void* ws /*nullable*/,
+                                  int64_t ws_bytes, gcg_stream_t stream);
+/* Workspace of gcg_gemm_nt_f32_bf16x6 (bytes, 16-B aligned): Bt's three planes, split once per
+ * call by a small kernel on the same stream, so the loop converts only A. ws == NULL splits
+ * both operands inside the loop instead (same products, bitwise). */
+int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K);
+
+/*
  * Fused output layer + loss (N <= 1024; one workgroup owns whole rows):
  *   logits = A . W + bias                                       mlpconv.py:88-93
  *   labels != NULL: out = (softmax(logits) - onehot(labels)) * scale   (the logits gradient

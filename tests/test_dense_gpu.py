@@ -314,11 +314,14 @@ def test_lds_b_gemm_equals_register_b_gemm(cuda, M, K, N, monkeypatch):
                                    (70, 300, 321), (96, 300, 930), (300, 930, 300),
                                    (31, 65, 1024), (50, 40, 1500), (300, 129, 4),
                                    (1000, 256, 300), (517, 33, 930)])
-def test_gemm_nt_vs_float64(cuda, M, K, N):
-    """gcg_gemm_nt_f32 (LDS-DMA staged, both operands k-contiguous): C = A . Bt^T."""
+@pytest.mark.parametrize("math", dense.NT_MATHS)
+def test_gemm_nt_vs_float64(cuda, M, K, N, math):
+    """gcg_gemm_nt_f32 (LDS-DMA staged, both operands k-contiguous): C = A . Bt^T; and the same
+    product on the bf16 matrix cores (gcg_gemm_nt_f32_bf16x6, pre-split weight planes or both
+    operands split in the loop) within the same float64 bar."""
     A, B = _rand((M, K), 11), _rand((K, N), 12)
     Bt = _padded(B, cuda, transpose=True)  # N x round4(K)
-    C = dense.gemm_nt(torch.from_numpy(A).to(cuda), Bt).cpu().numpy()
+    C = dense.gemm_nt(torch.from_numpy(A).to(cuda), Bt, math=math).cpu().numpy()
     _check_gemm(C, A, B)
 
 
@@ -334,20 +337,81 @@ def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
     M, K, N = 333, 301, 133
     A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
     C = dense.gemm_nt(torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True),
-                      bias=torch.from_numpy(b).to(cuda), act="relu").cpu().numpy()
+                      bias=torch.from_numpy(b).to(cuda), act="relu", math="f32").cpu().numpy()
     _check_gemm(C, A, B, bias=b, relu=True)
 
 
-def test_gemm_nt_padding_never_leaks(cuda):
+NT3_TILES = ["2,1,4,1,2", "2,1,4,1,3", "4,1,4,1,2", "2,2,4,1,2", "2,2,4,1,3", "2,1,2,2,2",
+             "4,1,2,2,2", "2,1,4,2,2", "2,1,4,2,3", "2,2,4,2,2", "4,1,4,2,2", "2,1,4,1,0",
+             "2,2,4,1,0", "4,1,4,1,0", "2,1,2,1,0", "2,2,2,1,0", "4,1,2,1,0", "2,1,4,2,0"]
+
+
+@pytest.mark.parametrize("M,K,N", [(333, 301, 133), (1000, 300, 930), (517, 930, 300),
+                                   (70, 33, 65), (1, 5, 3)])
+def test_gemm_nt_bf16x6_tiles_bitwise(cuda, M, K, N, monkeypatch):
+    """Every bf16x6 tile (GCG_NT3_CFG; S = 0: A in registers) and the in-loop split of both
+    operands accumulate the same six plane products in the same order: bitwise equal to each
+    other, with bias + relu, ragged M / N / K; within the float64 bar."""
+    A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
+    At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
+    bt = torch.from_numpy(b).to(cuda)
+    ref = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6_inloop")
+    _check_gemm(ref.cpu().numpy(), A, B, bias=b, relu=True)
+    for cfg in NT3_TILES:
+        monkeypatch.setenv("GCG_NT3_CFG", cfg)
+        C = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6")
+        assert torch.equal(C, ref), cfg
+
+
+def test_gemm_nt_bf16x6_error_at_most_f32s(cuda):
+    """The bf16x6 products are f32-accurate: on 4096 x 300 x 930 with operands spanning six
+    decades (sign-mixed, log-uniform magnitudes), the largest error against float64 relative to
+    sum_k |a||b| is within 1.25 x the f32 MFMA kernel's, and below 2^-20."""
+    rng = np.random.default_rng(40)
+    M, K, N = 4096, 300, 930
+    A = (rng.choice([-1.0, 1.0], (M, K)) * 10.0 ** rng.uniform(-3, 3, (M, K))).astype(np.float32)
+    B = (rng.choice([-1.0, 1.0], (K, N)) * 10.0 ** rng.uniform(-3, 3, (K, N))).astype(np.float32)
+    At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
+    C64 = A.astype(np.float64) @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+    rel = {}
+    for math in ("f32", "bf16x6"):
+        C = dense.gemm_nt(At, Bt, math=math).cpu().numpy().astype(np.float64)
+        rel[math] = float((np.abs(C - C64) / scale).max())
+    assert rel["bf16x6"] <= 1.25 * rel["f32"] and rel["bf16x6"] < 2.0 ** -20, rel
+
+
+def test_gemm_nt_bf16x6_nan_propagates(cuda):
+    """A NaN operand element reaches exactly the outputs whose dot product it enters."""
+    M, K, N = 64, 100, 70
+    A, B = _rand((M, K), 41), _rand((K, N), 42)
+    A[5, 17] = np.nan
+    B[33, 9] = np.nan
+    for math in ("bf16x6", "bf16x6_inloop"):
+        C = dense.gemm_nt(torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True),
+                          math=math).cpu().numpy()
+        bad = np.zeros((M, N), bool)
+        bad[5, :] = True
+        bad[:, 9] = True
+        assert np.array_equal(np.isnan(C), bad), math
+
+
+@pytest.mark.parametrize("math", dense.NT_MATHS)
+@pytest.mark.parametrize("tile", [None, "2,1,4,1,2", "2,2,4,1,0"])
+def test_gemm_nt_padding_never_leaks(cuda, math, tile, monkeypatch):
     """The k tail is zeroed in the fragments: NaN in the operands' padding columns (k >= K, inside
     the row stride) and in rows past M / N must not reach C."""
+    if tile is not None:
+        if math != "bf16x6":
+            pytest.skip("tile knob of the pre-split kernel")
+        monkeypatch.setenv("GCG_NT3_CFG", tile)
     M, K, N = 200, 298, 70
     A, B = _rand((M, K), 16), _rand((K, N), 17)
     Ap = torch.full((M, 300), float("nan"), device=cuda)
     Ap[:, :K] = torch.from_numpy(A).to(cuda)
     Btp = torch.full((N, 300), float("nan"), device=cuda)
     Btp[:, :K] = torch.from_numpy(B.T.copy()).to(cuda)
-    C = dense.gemm_nt(Ap[:, :K], Btp[:, :K]).cpu().numpy()
+    C = dense.gemm_nt(Ap[:, :K], Btp[:, :K], math=math).cpu().numpy()
     assert np.isfinite(C).all()
     _check_gemm(C, A, B)
 

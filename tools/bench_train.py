@@ -38,6 +38,8 @@ def main():
     ap.add_argument("--mode", default="auto")
     ap.add_argument("--order", default="reference", choices=["reference", "propagate_first", "auto"])
     ap.add_argument("--graph", action="store_true", help="replay the step as a captured HIP graph")
+    ap.add_argument("--nt-math", default=None, choices=["f32", "bf16x6", "bf16x6_inloop"],
+                    help="products of the NT GEMMs (dense.NT_MATH)")
     ap.add_argument("--legacy-stride", action="store_true",
                     help="round-3 row strides for wide operands (sparse.WIDE_ROW_ALIGN = False)")
     ap.add_argument("--inline-weight-grads", action="store_true",
@@ -46,6 +48,9 @@ def main():
                     help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
     args = ap.parse_args()
     gs.WIDE_ROW_ALIGN = not args.legacy_stride
+    from graphconvgeo_amd import dense
+    if args.nt_math:
+        dense.NT_MATH = args.nt_math
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
     if args.inline_weight_grads:
@@ -102,7 +107,8 @@ def main():
            "spmm_effective_GBps_if_all_time_in_spmm": round(total / (ms * 1e-3) / 1e9, 1),
            "mode": args.mode, "order": args.order, "hip_graph": args.graph,
            "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
-           "legacy_stride": args.legacy_stride, "data_gen_s": round(t_gen, 1)}
+           "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
+           "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
 
