@@ -518,6 +518,65 @@ def resolve_mode(A, mode: str) -> str:
     return mode if mode != "auto" else gs.resolve_auto(A)
 
 
+def alternatives(H, rank, world, dev, part, Zl, K, B, eff, gen, timed, reps, args) -> dict:
+    """Alternative strategies measured in the same N > 1 run: H replicated with Z split by columns
+    (no exchange, distributed.FeatureParallelSpMM), and the exchange A/B --
+    the same pipelined step with every exchange: RCCL all-gather (in place), a direct mesh of
+    isend/irecv pairs (every xGMI link at once), the halo all-to-all of only the referenced rows
+    -- and each exchange alone."""
+    from graphconvgeo_amd.distributed import FeatureParallelSpMM
+    N = H.shape[0]
+    fp = FeatureParallelSpMM(H, rank, world, dev, K)
+    Zc = torch.randn((N, fp.width), generator=gen, device=dev, dtype=torch.float32)
+    Yc = gs.empty_dense(N, fp.width, dev)
+    fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
+    for _ in range(args.warmup):
+        fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
+    t_fp = timed(lambda: fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz), args.steps)
+    alt = {"feature_parallel": {"ms_per_step": round(t_fp, 4),
+                                "value": round(B / (t_fp * 1e-3) / 1e9, 1), "unit": "GB/s",
+                                "columns_per_gpu": fp.width, "exchange": "none",
+                                "note": "H replicated (0.34 GB), Z/Y split by columns"}}
+    del fp, Zc, Yc
+    # The exchange A/B (SURVEY.md §5/§8e): the same pipelined step with every exchange --
+    # RCCL all-gather (in place), a direct mesh of isend/irecv pairs (every xGMI link at
+    # once), the halo all-to-all of only the referenced rows -- and each exchange alone.
+    for m in ("allgather", "mesh", "halo"):
+        try:
+            alt.update(exchange_ab(H, rank, world, dev, part, Zl, K, B, eff, timed, reps, args, m))
+        except Exception as exc:  # noqa: BLE001 -- one exchange failing keeps the others
+            alt[f"exchange_{m}"] = {"error": f"{type(exc).__name__}: {exc}"[:500]}
+        torch.cuda.empty_cache()
+    return alt
+
+
+def exchange_ab(H, rank, world, dev, part, Zl, K, B, eff, timed, reps, args, m) -> dict:
+    """One exchange of the A/B: the pipelined step with it, and the exchange alone."""
+    from graphconvgeo_amd.distributed import RowPartitionedCSR
+    alt = {}
+    pm = part if m == part.exchange else RowPartitionedCSR(H, rank, world, dev, exchange=m)
+    cm = pm._n_chunks(args.chunks, K)
+    pm.chunk_buffers(K, cm).fill(Zl)
+    Ym = gs.empty_dense(pm.n_local, K, dev)
+
+    def step_m():
+        pm.spmm_pipelined(None, Ym, n_chunks=cm, mode=eff, task_nnz=args.task_nnz)
+    for _ in range(max(args.warmup, 1)):
+        step_m()
+    t_m = timed(step_m, args.steps)
+    b1 = pm.chunk_buffers(K, 1)
+    b1.fill(Zl)
+    t_x = timed(lambda: pm.layout.exchange(b1.chunks[0][2], async_op=False), reps)
+    alt[f"exchange_{m}_ms"] = round(t_m, 4)
+    alt[f"exchange_{m}"] = {"step_ms": round(t_m, 4), "exchange_alone_ms": round(t_x, 4),
+                            "chunks": cm, "bytes_in_per_gpu": pm.exchange_bytes_per_row(K),
+                            "value": round(B / (t_m * 1e-3) / 1e9, 1)}
+    if pm is not part:
+        del pm
+    del Ym
+    return alt
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -736,45 +795,14 @@ def main():
     # no exchange (distributed.FeatureParallelSpMM). Reported beside the row-partitioned value.
     alt = None
     if world > 1 and args.alternatives:
-        from graphconvgeo_amd.distributed import FeatureParallelSpMM
-        fp = FeatureParallelSpMM(H, rank, world, dev, K)
-        Zc = torch.randn((N, fp.width), generator=gen, device=dev, dtype=torch.float32)
-        Yc = gs.empty_dense(N, fp.width, dev)
-        fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
-        for _ in range(args.warmup):
-            fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz)
-        t_fp = timed(lambda: fp.spmm(Zc, out=Yc, mode=args.mode, task_nnz=args.task_nnz), args.steps)
-        alt = {"feature_parallel": {"ms_per_step": round(t_fp, 4),
-                                    "value": round(B / (t_fp * 1e-3) / 1e9, 1), "unit": "GB/s",
-                                    "columns_per_gpu": fp.width, "exchange": "none",
-                                    "note": "H replicated (0.34 GB), Z/Y split by columns"}}
-        del fp, Zc, Yc
-        # The exchange A/B: the same pipelined step with every exchange --
-        # RCCL all-gather (in place), a direct mesh of isend/irecv pairs (every xGMI link at
-        # once), the halo all-to-all of only the referenced rows -- and each exchange alone.
-        for m in ("allgather", "mesh", "halo"):
-            pm = part if m == part.exchange else RowPartitionedCSR(H, rank, world, dev, exchange=m)
-            cm = pm._n_chunks(args.chunks, K)
-            pm.chunk_buffers(K, cm).fill(Zl)
-            Ym = gs.empty_dense(pm.n_local, K, dev)
+        try:
+            alt = alternatives(H, rank, world, dev, part, Zl, K, B, eff, gen, timed, reps, args)
+        except Exception as exc:  # noqa: BLE001 -- the A/B is an extra: keep the line
+            # (raised on every rank alike -- a bad argument, an unsupported op -- so no rank is
+            # left waiting in a collective)
+            alt = {"error": f"{type(exc).__name__}: {exc}"[:500]}
 
-            def step_m():
-                pm.spmm_pipelined(None, Ym, n_chunks=cm, mode=eff, task_nnz=args.task_nnz)
-            for _ in range(max(args.warmup, 1)):
-                step_m()
-            t_m = timed(step_m, args.steps)
-            b1 = pm.chunk_buffers(K, 1)
-            b1.fill(Zl)
-            t_x = timed(lambda: pm.layout.exchange(b1.chunks[0][2], async_op=False), reps)
-            alt[f"exchange_{m}_ms"] = round(t_m, 4)
-            alt[f"exchange_{m}"] = {"step_ms": round(t_m, 4), "exchange_alone_ms": round(t_x, 4),
-                                    "chunks": cm, "bytes_in_per_gpu": pm.exchange_bytes_per_row(K),
-                                    "value": round(B / (t_m * 1e-3) / 1e9, 1)}
-            if pm is not part:
-                del pm
-            del Ym
-            torch.cuda.empty_cache()
-
+    value = B / (ms * 1e-3) / 1e9
     value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
