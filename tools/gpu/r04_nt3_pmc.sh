@@ -2,7 +2,7 @@
 # Round 4: PMC passes over the bf16x6 pre-split NT GEMM, two tiles.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-for cfg in "2,1,4,1,2" "2,2,4,1,2"; do
+for cfg in ${NT3_CFGS:-"2,1,4,1,2" "2,2,4,1,2"}; do
   tag=$(echo $cfg | tr ',' '_')
   GCG_NT3_CFG=$cfg OUT=gpurun_out/r04/nt3pmc/$tag DRIVER=tools/exp_nt3_one.py bash tools/gpu/pmc_nt.sh > /dev/null || exit 1
   python3 tools/pmc_dense_summary.py gpurun_out/r04/nt3pmc/$tag --out gpurun_out/r04/nt3pmc/$tag.json > /dev/null || exit 1
