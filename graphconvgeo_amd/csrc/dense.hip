@@ -31,6 +31,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstring>
 #include <limits>
 
 #include "common.h"
@@ -1270,6 +1271,202 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 #undef GCG_EPI_BV_READY
 }
 
+// ---------------------------------------------------------------------------------------
+// gemm_fused6_kernel<RT, G>: the fused output layer (gemm_kernel EPI = 1: P . W + b -> softmax,
+// cross-entropy, hits, logits gradient / probabilities) with the products on the bf16 matrix
+// cores (bf16x6, as gcg_gemm_nt_f32_bf16x6; round 4). A workgroup owns 16 RT whole rows: 4
+// waves x 64 G columns (N <= 256 G). A goes through the LDS-DMA ring (the nt3 image: [BM][8
+// slots], key r & 7; each wave reads all rows) and is split in registers; the weight W
+// (K x N, L2-resident) is read straight into registers as f32, one dwordx4 of 4 adjacent columns
+// per lane and k row -- rows k0 + 4q + i and k0 + 16 + 4q + i (i < 4) give, per column, the 8
+// k-values of the lane's bf16 operand in the A image's k order -- and split in registers; the
+// next 64-column group's 8 loads are in flight while a group computes. Weight rows past K read
+// as 0 (buffer range), A's elements past K are zeroed before the split, W's padding columns
+// are handled by the epilogue's straddle guard. All LDS (ring, row reductions, bias, labels,
+// row weights) is one array: a second __shared__ object makes hipcc drain the DMA queue.
+// ---------------------------------------------------------------------------------------
+template <int RT, int G>
+__global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
+    int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+    int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
+    const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
+    float* __restrict__ loss_rows, float* __restrict__ correct_rows,
+    const float* __restrict__ row_w) {
+  constexpr int WR = 1, WC = 4, EPI = 1, S = 2;
+  constexpr int BM = 16 * RT, BN = 64 * G * WC;
+  constexpr int STAGE = BM * 32;                 // A image floats per stage
+  constexpr int NGA = BM / 8;                    // A DMA wave-instructions per stage
+  static_assert(NGA % WC == 0, "whole A DMA instructions per wave");
+  constexpr int UA = NGA / WC;
+  constexpr int OFF_RED = S * STAGE, OFF_BIAS = OFF_RED + 4 * WC * BM;
+  constexpr int OFF_LAB = OFF_BIAS + BN, OFF_RW = OFF_LAB + BM;
+  __shared__ __attribute__((aligned(16))) float smem[OFF_RW + BM];
+  float (*red)[WC][BM] = reinterpret_cast<float (*)[WC][BM]>(smem + OFF_RED);
+  float* sbias = smem + OFF_BIAS;
+  int* slab = reinterpret_cast<int*>(smem + OFF_LAB);
+  float* srw = smem + OFF_RW;
+  const int act = GCG_ACT_NONE;
+  (void)act;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = 0, wc = wave;
+  const int j = lane & 15, q = lane >> 4;
+  const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
+  const int colw = wc * G * 64;
+  const int Kc = (K + 31) / 32;
+  const int rows_here = static_cast<int>(M - row0 < BM ? M - row0 : BM);
+  const int n4 = (N + 3) & ~3;
+
+  // A DMA: instruction i = wave + WC u fills image rows 8i .. 8i + 7
+  int voff[UA];
+#pragma unroll
+  for (int u = 0; u < UA; ++u) {
+    const int r = 8 * (wave + WC * u) + lane / 8;
+    const int rl = r < rows_here ? r : rows_here - 1;
+    voff[u] = (rl * static_cast<int>(lda) + 4 * ((lane % 8) ^ (r & 7))) * 4;
+  }
+  const int a_bytes = ((rows_here - 1) * static_cast<int>(lda) + ((K + 3) & ~3)) * 4;
+  auto issue_a = [&](int chunk) {
+    float* stage = smem + (chunk & 1) * STAGE;
+    const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
+#pragma unroll
+    for (int u = 0; u < UA; ++u) blds16(ra, stage + (wave + WC * u) * 256, voff[u]);
+  };
+  // W: lane offsets (row 4q, column of group g); rows i and 16 + i through the scalar offset
+  int bofs[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const int c = colw + 64 * g + 4 * j;
+    bofs[g] = ((4 * q) * static_cast<int>(ldb) + (c < n4 ? c : 0)) * 4;
+  }
+  const int ldb4 = static_cast<int>(ldb) * 4;
+  auto load_w = [&](int chunk, int g, f4 (&w)[8]) {
+    const int k0 = 32 * chunk;
+    const auto rw = brsrc(B + static_cast<int64_t>(k0) * ldb, (K - k0) * ldb4);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      w[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rw, bofs[g], i * ldb4, 0));
+      w[4 + i] = __builtin_bit_cast(
+          f4, __builtin_amdgcn_raw_buffer_load_b128(rw, bofs[g], (16 + i) * ldb4, 0));
+    }
+  };
+
+  f4 acc[RT][G][4];
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+
+  for (int c = tid; c < BN; c += 64 * WC)  // columns past N: -inf (softmax weight exactly 0)
+    sbias[c] = c < N ? (bias != nullptr ? bias[c] : 0.f) : kNegInf;
+  for (int r = tid; r < BM; r += 64 * WC) {
+    const int64_t row = row0 + r;
+    int y = (labels != nullptr && row < M) ? labels[row] : -1;
+    if (labels != nullptr && (y < 0 || y >= N)) y = -2;  // outside [0, N): NaN loss, no hit
+    slab[r] = y;
+    srw[r] = (row_w != nullptr && row < M) ? row_w[row] : 1.f;
+  }
+
+  const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
+  const int arow0 = j;
+  f4 w0[8], w1[8];
+  issue_a(0);
+  if (ngv > 0) load_w(0, 0, w0);
+  auto group = [&](int c, int g, const bf8 (&ap)[RT][3], const f4 (&w)[8], f4 (&wn)[8]) {
+    // prefetch the next group (or the next chunk's first) into the other set
+    if (g + 1 < ngv) load_w(c, g + 1, wn);
+    else if (c + 1 < Kc && ngv > 0) load_w(c + 1, 0, wn);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f8 y = {w[0][e], w[1][e], w[2][e], w[3][e], w[4][e], w[5][e], w[6][e], w[7][e]};
+      bf8 b0, b1, b2;
+      split3(y, b0, b1, b2);
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        f4 cc = acc[t][g][e];
+        cc = mfma_bf(ap[t][2], b0, cc);
+        cc = mfma_bf(ap[t][1], b1, cc);
+        cc = mfma_bf(ap[t][0], b2, cc);
+        cc = mfma_bf(ap[t][1], b0, cc);
+        cc = mfma_bf(ap[t][0], b1, cc);
+        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+      }
+    }
+  };
+  // one chunk; wa holds its first group's W on entry. G even: the next chunk's first group
+  // ends in wa again, G odd (G = 1, 3): in wb, so the loop alternates the sets (a wave whose
+  // live-group count has the other parity -- it straddles N -- moves it)
+  auto chunk = [&](int c, f4 (&wa)[8], f4 (&wb)[8]) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A(c) landed (and W's prefetch)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (c + 1 < Kc) issue_a(c + 1);
+    const int kc0 = 32 * c;
+    const float* stage = smem + (c & 1) * STAGE;
+    bf8 ap[RT][3];
+#pragma unroll
+    for (int t = 0; t < RT; ++t) {
+      const int r = arow0 + 16 * t;
+      const f4 lo = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * (q ^ (r & 7)));
+      const f4 hi = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * ((4 + q) ^ (r & 7)));
+      f8 x = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+      if (kc0 + 32 > K) {
+        const int lim = K - kc0 - 4 * q;
+#pragma unroll
+        for (int w = 0; w < 4; ++w) {
+          x[w] = w < lim ? x[w] : 0.f;
+          x[4 + w] = 16 + w < lim ? x[4 + w] : 0.f;
+        }
+      }
+      split3(x, ap[t][0], ap[t][1], ap[t][2]);
+    }
+#pragma unroll
+    for (int g = 0; g < G; ++g) {
+      if (g >= ngv) break;  // wave-uniform: groups wholly past N
+      if (g % 2 == 0) {
+        group(c, g, ap, wa, wb);
+      } else {
+        group(c, g, ap, wb, wa);
+      }
+    }
+    // the last live group (ngv - 1) prefetched the next chunk's first into wb when ngv is odd
+    if (ngv > 0 && c + 1 < Kc) {
+      const bool in_b = (ngv & 1) != 0;
+      if constexpr (G % 2 == 0) {
+        if (in_b) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) wa[i] = wb[i];
+        }
+      } else {
+        if (!in_b) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) wb[i] = wa[i];
+        }
+      }
+    }
+  };
+  if constexpr (G % 2 == 0) {
+    for (int c = 0; c < Kc; ++c) chunk(c, w0, w1);
+  } else {
+    for (int c = 0; c < Kc; c += 2) {
+      chunk(c, w0, w1);
+      if (c + 1 < Kc) chunk(c + 1, w1, w0);
+    }
+  }
+#define GCG_EPI_BV_READY
+#define GCG_EPI_LABELS_LDS
+  f4 bv[G];
+#pragma unroll
+  for (int g = 0; g < G; ++g) bv[g] = *reinterpret_cast<const f4*>(&sbias[colw + 64 * g + 4 * j]);
+#include "gemm_epilogue.inc"
+#undef GCG_EPI_BV_READY
+#undef GCG_EPI_LABELS_LDS
+}
+
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
 // exp, label logit and first-index argmax, then dlogits / probabilities. In-place safe.
 template <int NV>
@@ -1736,6 +1933,35 @@ gcg_status check_dense(const char* fn, const float* p, int64_t ld, int64_t cols,
   return GCG_OK;
 }
 
+// The fused output layer on the bf16 matrix cores (gemm_fused6_kernel): 32 whole rows per
+// workgroup, G = ceil(N / 256) column groups per wave. GCG_FUSED_MATH=f32 keeps gemm_kernel.
+bool fused_bf16x6() {
+  const char* v = std::getenv("GCG_FUSED_MATH");
+  return !(v && std::strcmp(v, "f32") == 0);
+}
+gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, const float* B,
+                         int64_t ldb, const float* bias, float* C, int64_t ldc,
+                         const int32_t* labels, float scale, const float* scale_dev,
+                         float* loss_rows, float* correct_rows, const float* row_w,
+                         hipStream_t st) {
+  const int g = (N + 255) / 256;
+  const dim3 grid(static_cast<unsigned>((M + 31) / 32));
+#define GCG_FUSED6_CASE(g_)                                                                    \
+  if (g == g_) {                                                                              \
+    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_>), grid, dim3(256), 0, st, int(M), N, K, A,  \
+                       lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows,        \
+                       correct_rows, row_w);                                                  \
+    GCG_HIP_CHECK(hipGetLastError());                                                         \
+    return GCG_OK;                                                                            \
+  }
+  GCG_FUSED6_CASE(1)
+  GCG_FUSED6_CASE(2)
+  GCG_FUSED6_CASE(3)
+  GCG_FUSED6_CASE(4)
+#undef GCG_FUSED6_CASE
+  return fail(GCG_ERR_INVALID_ARG, "fused layer: N=%d", N);
+}
+
 gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t K,
                        const float* A, int64_t lda, const float* B, int64_t ldb,
                        const float* bias, int act, float* C, int64_t ldc,
@@ -1771,6 +1997,9 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
             static_cast<unsigned>((N + sh.bn() - 1) / sh.bn()));
   if (grid.x > 0x7fffffffu) return fail(GCG_ERR_INVALID_ARG, "%s: M too large", fn);
   auto st = static_cast<hipStream_t>(stream);
+  if (fused && fused_bf16x6())
+    return launch_fused6(M, int(N), int(K), A, lda, B, ldb, bias, C, ldc, labels, scale,
+                         scale_dev, loss_rows, correct_rows, row_w, st);
   if (fused)
     return launch_gemm<1>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
                           labels, scale, scale_dev, loss_rows, correct_rows, row_w);

@@ -89,8 +89,12 @@ def test_gemm_rejects_bad_operands(cuda):
 
 @pytest.mark.parametrize("M,K,N", [(1, 4, 2), (37, 16, 129), (300, 300, 256), (513, 300, 930),
                                    (64, 65, 1024), (20, 3, 61), (40, 50, 300), (33, 70, 700),
-                                   (20, 16, 700), (9, 4, 520)])
-def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
+                                   (20, 16, 700), (9, 4, 520), (70, 300, 600)])
+@pytest.mark.parametrize("math", ["bf16x6", "f32"])
+def test_fused_softmax_xent_vs_float64(cuda, M, K, N, math, monkeypatch):
+    """The fused output layer, on the bf16 matrix cores (gemm_fused6_kernel, the default) and on
+    the f32 MFMA (GCG_FUSED_MATH=f32, gemm_kernel): loss, gradient, hits, probabilities."""
+    monkeypatch.setenv("GCG_FUSED_MATH", math)
     P, W, b = _rand((M, K), 11, 0.3), _rand((K, N), 12, 0.3), _rand((N,), 13)
     y = np.random.default_rng(14).integers(0, N, M).astype(np.int32)
     proj = dense.Projection()
@@ -117,10 +121,12 @@ def test_fused_softmax_xent_vs_float64(cuda, M, K, N):
 
 
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (20, 3, 61), (9, 4, 522),
-                                   (40, 50, 300)])
-def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N):
+                                   (40, 50, 300), (70, 300, 600)])
+@pytest.mark.parametrize("math", ["bf16x6", "f32"])
+def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N, math, monkeypatch):
     """W's padding columns [N, ldw) may hold anything (gcg_spmm.h): NaN there must not reach
     the softmax sum, the loss or the gradient -- bitwise the zero-padded result."""
+    monkeypatch.setenv("GCG_FUSED_MATH", math)
     P, W, b = _rand((M, K), 31, 0.3), _rand((K, N), 32, 0.3), _rand((N,), 33)
     y = np.random.default_rng(34).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
@@ -146,7 +152,9 @@ def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N):
                                    (40, 50, 300), (33, 70, 700), (65, 17, 900)])
 def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
     """The B ping-pong split (GCG_GEMM_SPLIT = 0 / 2 / 4 / 8 / 16 register-set parts) only reorders
-    MFMAs between distinct accumulators: gradient, loss and hits are bitwise equal."""
+    MFMAs between distinct accumulators: gradient, loss and hits are bitwise equal (the f32 MFMA
+    kernel, GCG_FUSED_MATH=f32)."""
+    monkeypatch.setenv("GCG_FUSED_MATH", "f32")
     P, W, b = _rand((M, K), 21, 0.3), _rand((K, N), 22, 0.3), _rand((N,), 23)
     y = np.random.default_rng(24).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))

@@ -4,7 +4,8 @@ MFMA launch (gcg_project_softmax_xent_weighted_f32) against the composition bf16
 (logits into G) + the row softmax-CE kernel in place (gcg_softmax_xent_weighted_f32): the
 composition pays one more logits round trip through HBM and gains the bf16 matrix cores.
 World (840k x 300 x 930) and Twitter-US (270k x 300 x 256) target shapes; HIP events, mean of
-10, interleaved rounds; outputs compared (G max abs diff, loss / hits)."""
+10, interleaved rounds; outputs compared (G max abs diff, loss / hits). Round 4, later: also the
+fused layer on the bf16 matrix cores (gemm_fused6_kernel, GCG_FUSED_MATH=bf16x6)."""
 import json
 import math
 import os
@@ -44,7 +45,12 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     h1, h2 = torch.empty(T, device=dev), torch.empty(T, device=dev)
 
     def fused():
+        os.environ["GCG_FUSED_MATH"] = "f32"
         dense._fused(P, Wp, b, y, 1.0 / T, None, G1, l1, h1)
+
+    def fused6():
+        os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
 
     def compose():
         dense.gemm_nt(P, Wt, bias=b, out=G2, math="bf16x6")
@@ -55,9 +61,14 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     torch.cuda.synchronize()
     rec = {"shape": f"{T}x{K}x{C}", "G_maxdiff": float((G1 - G2).abs().max()),
            "loss_maxdiff": float((l1 - l2).abs().max()), "hits_diff": float((h1 - h2).abs().sum())}
+    fused6()
+    torch.cuda.synchronize()
+    rec.update(G_maxdiff_fused6=float((G1 - G2).abs().max()),
+               loss_maxdiff_fused6=float((l1 - l2).abs().max()),
+               hits_diff_fused6=float((h1 - h2).abs().sum()))
     flops = 2.0 * T * K * C
     for rnd in range(3):
-        for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose)):
+        for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose), ("fused_bf16x6", fused6)):
             ms = timeit(fn)
             rec.setdefault(name, []).append([round(ms, 3), round(flops / ms / 1e9, 1)])
     print(json.dumps(rec), flush=True)
