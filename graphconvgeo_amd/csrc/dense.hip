@@ -1285,19 +1285,19 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // are handled by the epilogue's straddle guard. All LDS (ring, row reductions, bias, labels,
 // row weights) is one array: a second __shared__ object makes hipcc drain the DMA queue.
 // ---------------------------------------------------------------------------------------
-template <int RT, int G>
-__global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
+template <int RT, int G, int WR = 1>
+__global__ __launch_bounds__(256 * WR, WR == 1 ? 2 : 1) void gemm_fused6_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
     float* __restrict__ loss_rows, float* __restrict__ correct_rows,
     const float* __restrict__ row_w) {
-  constexpr int WR = 1, WC = 4, EPI = 1, S = 2;
-  constexpr int BM = 16 * RT, BN = 64 * G * WC;
+  constexpr int WC = 4, EPI = 1, S = 2;
+  constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   constexpr int STAGE = BM * 32;                 // A image floats per stage
   constexpr int NGA = BM / 8;                    // A DMA wave-instructions per stage
-  static_assert(NGA % WC == 0, "whole A DMA instructions per wave");
-  constexpr int UA = NGA / WC;
+  constexpr int UA = NGA / (WR * WC);
+  static_assert(NGA % (WR * WC) == 0, "whole A DMA instructions per wave");
   constexpr int OFF_RED = S * STAGE, OFF_BIAS = OFF_RED + 4 * WC * BM;
   constexpr int OFF_LAB = OFF_BIAS + BN, OFF_RW = OFF_LAB + BM;
   __shared__ __attribute__((aligned(16))) float smem[OFF_RW + BM];
@@ -1311,7 +1311,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = 0, wc = wave;
+  const int wr = wave / WC, wc = wave % WC;
   const int j = lane & 15, q = lane >> 4;
   const int64_t row0 = static_cast<int64_t>(blockIdx.x) * BM;
   const int colw = wc * G * 64;
@@ -1323,7 +1323,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
   int voff[UA];
 #pragma unroll
   for (int u = 0; u < UA; ++u) {
-    const int r = 8 * (wave + WC * u) + lane / 8;
+    const int r = 8 * (wave + WR * WC * u) + lane / 8;
     const int rl = r < rows_here ? r : rows_here - 1;
     voff[u] = (rl * static_cast<int>(lda) + 4 * ((lane % 8) ^ (r & 7))) * 4;
   }
@@ -1332,7 +1332,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
     float* stage = smem + (chunk & 1) * STAGE;
     const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
 #pragma unroll
-    for (int u = 0; u < UA; ++u) blds16(ra, stage + (wave + WC * u) * 256, voff[u]);
+    for (int u = 0; u < UA; ++u) blds16(ra, stage + (wave + WR * WC * u) * 256, voff[u]);
   };
   // W: lane offsets (row 4q, column of group g); rows i and 16 + i through the scalar offset
   int bofs[G];
@@ -1361,9 +1361,9 @@ __global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
 #pragma unroll
       for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
 
-  for (int c = tid; c < BN; c += 64 * WC)  // columns past N: -inf (softmax weight exactly 0)
+  for (int c = tid; c < BN; c += 64 * WR * WC)  // columns past N: -inf (softmax weight 0)
     sbias[c] = c < N ? (bias != nullptr ? bias[c] : 0.f) : kNegInf;
-  for (int r = tid; r < BM; r += 64 * WC) {
+  for (int r = tid; r < BM; r += 64 * WR * WC) {
     const int64_t row = row0 + r;
     int y = (labels != nullptr && row < M) ? labels[row] : -1;
     if (labels != nullptr && (y < 0 || y >= N)) y = -2;  // outside [0, N): NaN loss, no hit
@@ -1372,7 +1372,7 @@ __global__ __launch_bounds__(256, 2) void gemm_fused6_kernel(
   }
 
   const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
-  const int arow0 = j;
+  const int arow0 = wr * 16 * RT + j;
   f4 w0[8], w1[8];
   issue_a(0);
   if (ngv > 0) load_w(0, 0, w0);
@@ -1945,19 +1945,24 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
                          float* loss_rows, float* correct_rows, const float* row_w,
                          hipStream_t st) {
   const int g = (N + 255) / 256;
-  const dim3 grid(static_cast<unsigned>((M + 31) / 32));
-#define GCG_FUSED6_CASE(g_)                                                                    \
-  if (g == g_) {                                                                              \
-    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_>), grid, dim3(256), 0, st, int(M), N, K, A,  \
-                       lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows,        \
-                       correct_rows, row_w);                                                  \
+  const int wr = env_int("GCG_FUSED6_WR") == 2 ? 2 : 1;  // experiment: 2 row bands (8 waves)
+  const dim3 grid(static_cast<unsigned>((M + 32 * wr - 1) / (32 * wr)));
+#define GCG_FUSED6_CASE(g_, wr_)                                                               \
+  if (g == g_ && wr == wr_) {                                                                 \
+    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_, wr_>), grid, dim3(256 * wr_), 0, st, int(M), \
+                       N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev,          \
+                       loss_rows, correct_rows, row_w);                                       \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
-  GCG_FUSED6_CASE(1)
-  GCG_FUSED6_CASE(2)
-  GCG_FUSED6_CASE(3)
-  GCG_FUSED6_CASE(4)
+  GCG_FUSED6_CASE(1, 1)
+  GCG_FUSED6_CASE(2, 1)
+  GCG_FUSED6_CASE(3, 1)
+  GCG_FUSED6_CASE(4, 1)
+  GCG_FUSED6_CASE(1, 2)
+  GCG_FUSED6_CASE(2, 2)
+  GCG_FUSED6_CASE(3, 2)
+  GCG_FUSED6_CASE(4, 2)
 #undef GCG_FUSED6_CASE
   return fail(GCG_ERR_INVALID_ARG, "fused layer: N=%d", N);
 }

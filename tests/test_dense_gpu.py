@@ -172,6 +172,31 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
         assert torch.equal(hits, outs[0][2])
 
 
+@pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
+                                   (9, 4, 61)])
+def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
+    """gemm_fused6_kernel with two row bands per workgroup (GCG_FUSED6_WR=2, 8 waves) runs the
+    same products in the same order per element: bitwise the 4-wave kernel (gradient, loss,
+    hits, probabilities), rows past M included."""
+    monkeypatch.setenv("GCG_FUSED_MATH", "bf16x6")
+    P, W, b = _rand((M, K), 51, 0.3), _rand((K, N), 52, 0.3), _rand((N,), 53)
+    y = np.random.default_rng(54).integers(0, N, M).astype(np.int32)
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    Wp = dense.Projection().fwd.get(Wt, False)
+    outs = []
+    for wr in ("1", "2"):
+        monkeypatch.setenv("GCG_FUSED6_WR", wr)
+        G = empty_dense(M, N, cuda)
+        loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
+        probs = empty_dense(M, N, cuda)
+        dense._fused(Pt, Wp, bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None)
+        outs.append((G, loss, hits, probs))
+    for a, ref in zip(outs[1], outs[0]):
+        assert torch.equal(a, ref)
+
+
 def test_rows_softmax_xent_vs_float64(cuda):
     for M, N in [(1, 1), (9, 3), (1000, 930), (257, 256), (33, 4096), (5, 1025)]:
         L = _rand((M, N), M + N, 3.0)

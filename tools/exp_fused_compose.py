@@ -50,6 +50,12 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
 
     def fused6():
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        os.environ.pop("GCG_FUSED6_WR", None)
+        dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
+
+    def fused6_wr2():
+        os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        os.environ["GCG_FUSED6_WR"] = "2"
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
 
     def compose():
@@ -68,7 +74,8 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
                hits_diff_fused6=float((h1 - h2).abs().sum()))
     flops = 2.0 * T * K * C
     for rnd in range(3):
-        for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose), ("fused_bf16x6", fused6)):
+        for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose), ("fused_bf16x6", fused6),
+                         ("fused_bf16x6_8waves", fused6_wr2)):
             ms = timeit(fn)
             rec.setdefault(name, []).append([round(ms, 3), round(flops / ms / 1e9, 1)])
     print(json.dumps(rec), flush=True)
