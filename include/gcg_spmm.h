@@ -385,6 +385,9 @@ int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K);
  * out needs ldo % 4 == 0 and a 16-B aligned base; its padding columns [N, round4(N)) are
  * written with zeros (whole dwordx4 row stores). W's padding columns [N, ldw) may hold
  * anything (NaN included): they never reach a logit.
+ * Products (round 4): on the bf16 matrix cores at f32 accuracy (three bf16 planes per f32
+ * operand, six plane products, as gcg_gemm_nt_f32_bf16x6); the environment variable
+ * GCG_FUSED_MATH=f32 selects the f32 MFMA kernel (v_mfma_f32_16x16x4_f32).
  */
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
                                         int64_t lda, const float* W, int64_t ldw,
