@@ -19,7 +19,10 @@ Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
   gemm_tn(A, B)                   C = A^T . B, the weight gradient h^T . g: a split-K MFMA kernel
                                   (reduction over ~10^6 rows), deterministic
 No product of the layer path goes to hipBLASLt / rocBLAS. There is no CPU path: CPU tensors
-raise.
+raise. Round 4: gemm_nt (NT_MATH) and the fused layer (GCG_FUSED_MATH) run their products on
+the bf16 matrix cores at f32 accuracy -- every f32 operand split into three bf16 planes, the six
+plane products of order <= 2^-16 accumulated in f32 ("bf16x6"; error against float64 at or
+below the f32 MFMA kernels', tests/test_dense_gpu.py); gemm_tn stays on the f32 MFMA.
 """
 from __future__ import annotations
 
