@@ -2166,9 +2166,25 @@ struct Nt3Shape {
 //   1.4M x 300 x 930           146          151-152     154-155  |             165-166  171      151
 //   450k x 300 x 256           138-141      155         154-155  |             155-157  168-170  141-142
 //   450k x 256 x 300           136          138-139     134-137  |             143-145  142      129
-// (deeper rings, S = 3, lost 15-30: one workgroup per CU). Default: register A, 128 x 128.
-Nt3Shape pick_nt3_shape() {
-  Nt3Shape sh{2, 2, 4, 1, 0};
+// (deeper rings, S = 3, lost 15-30: one workgroup per CU). Default: register A, 128 rows x
+// 64 G columns, G in 1..3 (the register-A rows of the table above are G = 1 / 2):
+//                       G = 1      G = 2      G = 3
+//   840k x 300 x 930    166-168    171-173    175-176   (N padded to 960 / 1024 / 960)
+//   840k x 930 x 300    162-163    166        170-172   (320 / 384 / 384)
+//   450k x 300 x 256    157-160    170-172    122       (256 / 256 / 384)
+//   450k x 256 x 300    144.5      142-144    137-138   (320 / 384 / 384)
+// Rule: the G padding N least (ties: the larger G -- fewer re-reads of A); for K > 512 the
+// largest G within 1.25 x the least padding (a long k loop amortises the wider tile's waste).
+Nt3Shape pick_nt3_shape(int64_t N, int64_t K) {
+  int64_t pad[4] = {0, 0, 0, 0}, least = INT64_MAX;
+  for (int g = 1; g <= 3; ++g) {
+    pad[g] = (N + 64 * g - 1) / (64 * g) * (64 * g);
+    least = std::min(least, pad[g]);
+  }
+  int best = 1;
+  for (int g = 1; g <= 3; ++g)
+    if (pad[g] == least || (K > 512 && 4 * pad[g] <= 5 * least)) best = g;
+  Nt3Shape sh{2, best, 4, 1, 0};
   if (const char* v = std::getenv("GCG_NT3_CFG")) {
     int a = 0, b = 0, c = 0, d = 0, e = 0;
     if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) == 5) sh = Nt3Shape{a, b, c, d, e};
@@ -2196,6 +2212,8 @@ gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const
     return launch_nt3r_t<rt_, g_, wr_, wc_>(a, Bs, st);
   GCG_NT3R_CASE(2, 1, 4, 1)
   GCG_NT3R_CASE(2, 2, 4, 1)
+  GCG_NT3R_CASE(2, 3, 4, 1)
+  GCG_NT3R_CASE(2, 3, 2, 1)
   GCG_NT3R_CASE(4, 1, 4, 1)
   GCG_NT3R_CASE(2, 1, 2, 1)
   GCG_NT3R_CASE(2, 2, 2, 1)
@@ -2246,7 +2264,7 @@ gcg_status gcg_gemm_nt_f32_bf16x6(int64_t M, int64_t N, int64_t K, const float* 
                      0, st, int(N), int(K), Kc, Bt, ldbt, static_cast<unsigned*>(ws));
   GCG_HIP_CHECK(hipGetLastError());
   NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
-  return launch_nt3(pick_nt3_shape(), st, a, static_cast<const unsigned*>(ws));
+  return launch_nt3(pick_nt3_shape(N, K), st, a, static_cast<const unsigned*>(ws));
 }
 
 }  // extern "C"

@@ -376,7 +376,8 @@ def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
 
 NT3_TILES = ["2,1,4,1,2", "2,1,4,1,3", "4,1,4,1,2", "2,2,4,1,2", "2,2,4,1,3", "2,1,2,2,2",
              "4,1,2,2,2", "2,1,4,2,2", "2,1,4,2,3", "2,2,4,2,2", "4,1,4,2,2", "2,1,4,1,0",
-             "2,2,4,1,0", "4,1,4,1,0", "2,1,2,1,0", "2,2,2,1,0", "4,1,2,1,0", "2,1,4,2,0"]
+             "2,2,4,1,0", "4,1,4,1,0", "2,1,2,1,0", "2,2,2,1,0", "4,1,2,1,0", "2,1,4,2,0",
+             "2,3,4,1,0", "2,3,2,1,0"]
 
 
 @pytest.mark.parametrize("M,K,N", [(333, 301, 133), (1000, 300, 930), (517, 930, 300),

@@ -57,7 +57,8 @@ def main():
             d = np.abs(C[rows].double().cpu().numpy() - ref)
             return float(d.max()), float((d / scale).max())
 
-        variants = [("f32", None), ("bf16x6_inloop", None)] + [("bf16x6", c) for c in args.cfgs.split(";")]
+        variants = [("f32", None), ("bf16x6_inloop", None), ("bf16x6", None)] + [
+            ("bf16x6", c) for c in args.cfgs.split(";") if c]
         for rnd in range(args.rounds):
             for math, cfg in variants:
                 if cfg is None:
