@@ -124,7 +124,7 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
 
 # gemm_nt's default products: "bf16x6" (round 4: f32 operands split into three bf16 planes on
 # the bf16 matrix cores, error against float64 at or below the f32 MFMA kernel's,
-# tests/test_dense_gpu.py; 164-171 vs 113-119 TFLOP/s at Twitter-World's shapes) or "f32"
+# tests/test_dense_gpu.py; 170-179 vs 113-119 TFLOP/s at Twitter-World's shapes) or "f32"
 # (v_mfma_f32_16x16x4_f32).
 NT_MATH = "bf16x6"
 NT_MATHS = ("f32", "bf16x6", "bf16x6_inloop")
