@@ -1694,123 +1694,6 @@ __global__ __launch_bounds__(WM <= 1 ? 256 : 64 * WM, (WM == 0 && OCC != 2) ? 1 
       }
 }
 
-// gemm_tn6_kernel<NG>: gemm_tn_partial_kernel (WM = 0, per-wave 64 x 64 NG tiles, 4 wave
-// tiles per workgroup, XCD remap, partials [split][Mp][Np] for gemm_tn_reduce_kernel) with the
-// products on the bf16 matrix cores (bf16x6, round 4). One step is 32 rows: lane (j, q) loads
-// rows t0 + 4q + i and t0 + 16 + 4q + i (i < 4) of A and B as dwordx4 (4 adjacent columns),
-// i.e. for each of the 4 column slots e the 8 k-values (rows) of its bf16 operand in one k
-// order shared by A and B; both are split in registers. Two register sets of loads (the step
-// loop unrolled by two): the next step's 8 (1 + NG) loads fly while a step computes. Rows past
-// the split read as 0 (buffer range). Accumulator layout = gemm_tn_partial_kernel's.
-template <int NG>
-__global__ __launch_bounds__(256, 1) void gemm_tn6_kernel(
-    int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
-    int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt,
-    int remap) {
-  const int lane = threadIdx.x & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int j = lane & 15, q = lane >> 4;
-  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
-  int tile = b;
-  if (remap) {
-    const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;
-    tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
-  }
-  const int wt = 4 * tile + wave;
-  const int bx = wt % mt, by = (wt / mt) % nt, bz = wt / (mt * nt);
-  const int m0 = bx * 64, n0 = by * (64 * NG);
-  if (n0 >= N || m0 >= M) return;
-  if (static_cast<int64_t>(bz) * rows_per_split >= R) return;
-  const int t_begin = bz * rows_per_split;
-  const int t_end = min(R, t_begin + rows_per_split);
-  const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
-  const int acol = (m0 + 4 * j < m4) ? m0 + 4 * j : 0;
-  int bcol[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) {
-    const int c = n0 + 64 * g + 4 * j;
-    bcol[g] = c < n4 ? c : 0;
-  }
-  f4 acc[4][NG][4];
-#pragma unroll
-  for (int a = 0; a < 4; ++a)
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc[a][g][e] = f4{0.f, 0.f, 0.f, 0.f};
-  // lane offsets of row 4q (the other 7 rows by the scalar offset)
-  const int aoff = (4 * q * static_cast<int>(lda) + acol) * 4;
-  int boff[NG];
-#pragma unroll
-  for (int g = 0; g < NG; ++g) boff[g] = (4 * q * static_cast<int>(ldb) + bcol[g]) * 4;
-  const int lda4 = static_cast<int>(lda) * 4, ldb4 = static_cast<int>(ldb) * 4;
-  auto load = [&](int t0, f4 (&ra)[8], f4 (&rb)[NG][8]) {
-    const int left = __builtin_amdgcn_readfirstlane(min(max(t_end - t0, 0), 32));
-    const int tb = __builtin_amdgcn_readfirstlane(left > 0 ? t0 : t_begin);
-    const auto ar = brsrc(A + static_cast<int64_t>(tb) * lda, left * lda4);
-    const auto br = brsrc(B + static_cast<int64_t>(tb) * ldb, left * ldb4);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const int row = i < 4 ? i : 12 + i;  // 4q + i, 16 + 4q + (i - 4)
-      ra[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ar, aoff, row * lda4, 0));
-#pragma unroll
-      for (int g = 0; g < NG; ++g)
-        rb[g][i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(br, boff[g], row * ldb4, 0));
-    }
-  };
-  auto compute = [&](const f4 (&ra)[8], const f4 (&rb)[NG][8]) {
-    bf8 ap[4][3];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const f8 x = {ra[0][e], ra[1][e], ra[2][e], ra[3][e], ra[4][e], ra[5][e], ra[6][e], ra[7][e]};
-      split3(x, ap[e][0], ap[e][1], ap[e][2]);
-    }
-#pragma unroll
-    for (int g = 0; g < NG; ++g)
-#pragma unroll
-      for (int eb = 0; eb < 4; ++eb) {
-        const f8 y = {rb[g][0][eb], rb[g][1][eb], rb[g][2][eb], rb[g][3][eb],
-                      rb[g][4][eb], rb[g][5][eb], rb[g][6][eb], rb[g][7][eb]};
-        bf8 b0, b1, b2;
-        split3(y, b0, b1, b2);
-#pragma unroll
-        for (int ea = 0; ea < 4; ++ea) {
-          f4 cc = acc[ea][g][eb];
-          cc = mfma_bf(ap[ea][2], b0, cc);
-          cc = mfma_bf(ap[ea][1], b1, cc);
-          cc = mfma_bf(ap[ea][0], b2, cc);
-          cc = mfma_bf(ap[ea][1], b0, cc);
-          cc = mfma_bf(ap[ea][0], b1, cc);
-          acc[ea][g][eb] = mfma_bf(ap[ea][0], b0, cc);
-        }
-      }
-  };
-  f4 ra0[8], rb0[NG][8], ra1[8], rb1[NG][8];
-  load(t_begin, ra0, rb0);
-  for (int t0 = t_begin; t0 < t_end; t0 += 64) {
-    load(t0 + 32, ra1, rb1);  // past t_end: an empty range, zeros (never computed)
-    compute(ra0, rb0);
-    if (t0 + 32 >= t_end) break;
-    load(t0 + 64, ra0, rb0);
-    compute(ra1, rb1);
-  }
-  // partial tile: lane holds C[m0 + 16q + 4r + ea][n0 + 64g + 4j + eb] in acc[ea][g][eb][r]
-  float* dst = part + static_cast<int64_t>(bz) * Mp * Np;
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int ea = 0; ea < 4; ++ea) {
-      const int m = m0 + 16 * q + 4 * r + ea;
-      float* row = dst + static_cast<int64_t>(m) * Np;
-#pragma unroll
-      for (int g = 0; g < NG; ++g) {
-        const int n = n0 + 64 * g + 4 * j;
-        *reinterpret_cast<f4*>(row + n) = f4{acc[ea][g][0][r], acc[ea][g][1][r],
-                                             acc[ea][g][2][r], acc[ea][g][3][r]};
-      }
-    }
-}
-
 // C[m][n] = scale * sum over the S split partials part[s][m][n], deterministic. One workgroup
 // per (row m, 64 column quads): wave w of the 8 sums the splits s = w, w + 8, ... (4 loads in
 // flight per lane), then the 8 wave sums are added in wave order through LDS. (One thread per
@@ -1863,14 +1746,8 @@ __global__ __launch_bounds__(64 * kTnRedWaves) void gemm_tn_reduce_kernel(
 
 struct TnPlan {
   int mg, ng, pd, wm = 1, occ = 0;  // tile variant (wm: waves stacked along M; occ: see kernel)
-  int bx6 = 0;                      // 1: gemm_tn6_kernel (bf16x6 products)
   int mt, nt, S, rows_per_split, Mp, Np;
 };
-
-bool tn_bf16x6() {
-  const char* v = std::getenv("GCG_TN_MATH");
-  return v && std::strcmp(v, "bf16x6") == 0;
-}
 
 TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   TnPlan p;
@@ -1897,9 +1774,6 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
   const bool stacked = M <= 256 && M % 64 == 0 && N <= 512;
   if (stacked) p.ng = 1, p.pd = 8, p.occ = 0, p.wm = static_cast<int>(M / 64), slots = 2048;
-  // bf16x6 products (gemm_tn6_kernel, GCG_TN_MATH=bf16x6): per-wave 64 x 128 tiles (64 x 64 for
-  // N <= 64), 1 wave per SIMD (two register sets of 32-row loads beside 128 accumulators)
-  if (!stacked && tn_bf16x6()) p.bx6 = 1, p.wm = 0, p.mg = 1, p.ng = N <= 64 ? 1 : 2, p.pd = 2, p.occ = 0, slots = 2048;
   // experiment knobs: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes
   // alone; GCG_TN_STACKED: a layout for the stacked shapes only)
   const char* v = std::getenv("GCG_TN");
@@ -1922,9 +1796,8 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   const int64_t max_s = std::max<int64_t>(1, R / 256);
   p.S = static_cast<int>(std::min(want, max_s));
   int64_t rps = (R + p.S - 1) / p.S;
-  const int align = p.bx6 ? 32 : 16;  // whole steps per split
-  rps = (rps + align - 1) / align * align;
-  p.rows_per_split = static_cast<int>(std::max<int64_t>(rps, align));
+  rps = (rps + 15) / 16 * 16;
+  p.rows_per_split = static_cast<int>(std::max<int64_t>(rps, 16));
   p.S = static_cast<int>((R + p.rows_per_split - 1) / p.rows_per_split);
   p.Mp = p.mt * tm;
   p.Np = p.nt * tn;
@@ -2532,8 +2405,6 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
     return GCG_OK;
   }
   const TnPlan p = tn_plan(R, M, N);
-  if (p.bx6 && (lda >= (int64_t{1} << 24) || ldb >= (int64_t{1} << 24)))  // 32-row ranges
-    return fail(GCG_ERR_INVALID_ARG, "%s: leading dimension too large for the bf16x6 tiles", fn);
   const size_t need = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
   if (workspace == nullptr || workspace_bytes < need)
     return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu bytes < %zu needed", fn, workspace_bytes,
@@ -2546,14 +2417,6 @@ gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int6
   const dim3 grid(static_cast<unsigned>(n_tiles));
   const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
   const int remap = rmv ? std::atoi(rmv) : 1;
-  if (p.bx6) {
-    if (p.ng == 1)
-      hipLaunchKernelGGL((gemm_tn6_kernel<1>), grid, dim3(256), 0, s, int(R), int(M), int(N), A,
-                         lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);
-    else
-      hipLaunchKernelGGL((gemm_tn6_kernel<2>), grid, dim3(256), 0, s, int(R), int(M), int(N), A,
-                         lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);
-  } else
 #define GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, OCC_)                                            \
   if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_ && p.occ == OCC_) {           \
     hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_, OCC_>), grid,             \

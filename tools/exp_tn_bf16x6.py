@@ -2,7 +2,8 @@
 """Split-K weight gradient C = A^T . B (gcg_gemm_tn_f32) with f32 MFMA products against the
 bf16x6 tiles (gemm_tn6_kernel, GCG_TN_MATH=bf16x6): dW2 = P^T . G at Twitter-World's and
 Twitter-US's shapes. HIP events, mean of 10, interleaved rounds; error on the whole output
-against float64, max |err| / (sum_r |a||b|)."""
+against float64, max |err| / (sum_r |a||b|). The kernel and knob were reverted after this A/B (no gain:
+profiles/r04/tn_bf16x6_ab.jsonl); they live in commit decb56f."""
 import json
 import os
 import sys
