@@ -1285,14 +1285,14 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // are handled by the epilogue's straddle guard. All LDS (ring, row reductions, bias, labels,
 // row weights) is one array: a second __shared__ object makes hipcc drain the DMA queue.
 // ---------------------------------------------------------------------------------------
-template <int RT, int G, int WR = 1>
-__global__ __launch_bounds__(256 * WR, WR == 1 ? 2 : 1) void gemm_fused6_kernel(
+template <int RT, int G, int WR = 1, int WC = 4, int SB = 0>
+__global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused6_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
     float* __restrict__ loss_rows, float* __restrict__ correct_rows,
     const float* __restrict__ row_w) {
-  constexpr int WC = 4, EPI = 1, S = 2;
+  constexpr int EPI = 1, S = 2;
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   constexpr int STAGE = BM * 32;                 // A image floats per stage
   constexpr int NGA = BM / 8;                    // A DMA wave-instructions per stage
@@ -1397,6 +1397,31 @@ __global__ __launch_bounds__(256 * WR, WR == 1 ? 2 : 1) void gemm_fused6_kernel(
       }
     }
   };
+  // SB = 1 (one W register set, for tiles whose accumulators leave no room for two): the next
+  // group's loads go into the set as soon as its last column slot is split, so they fly during
+  // that slot's MFMAs and the other waves' work
+  auto group_sb = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&w)[8]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const f8 y = {w[0][e], w[1][e], w[2][e], w[3][e], w[4][e], w[5][e], w[6][e], w[7][e]};
+      bf8 b0, b1, b2;
+      split3(y, b0, b1, b2);
+      if (e == 3) {
+        if (g + 1 < ngv) load_w(c, g + 1, w);
+        else if (c + 1 < Kc && ngv > 0) load_w(c + 1, 0, w);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        f4 cc = acc[t][g][e];
+        cc = mfma_bf(ap[t][2], b0, cc);
+        cc = mfma_bf(ap[t][1], b1, cc);
+        cc = mfma_bf(ap[t][0], b2, cc);
+        cc = mfma_bf(ap[t][1], b0, cc);
+        cc = mfma_bf(ap[t][0], b1, cc);
+        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+      }
+    }
+  };
   // one chunk; wa holds its first group's W on entry. G even: the next chunk's first group
   // ends in wa again, G odd (G = 1, 3): in wb, so the loop alternates the sets (a wave whose
   // live-group count has the other parity -- it straddles N -- moves it)
@@ -1427,14 +1452,16 @@ __global__ __launch_bounds__(256 * WR, WR == 1 ? 2 : 1) void gemm_fused6_kernel(
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (g >= ngv) break;  // wave-uniform: groups wholly past N
-      if (g % 2 == 0) {
+      if constexpr (SB) {
+        group_sb(c, g, ap, wa);
+      } else if (g % 2 == 0) {
         group(c, g, ap, wa, wb);
       } else {
         group(c, g, ap, wb, wa);
       }
     }
     // the last live group (ngv - 1) prefetched the next chunk's first into wb when ngv is odd
-    if (ngv > 0 && c + 1 < Kc) {
+    if (!SB && ngv > 0 && c + 1 < Kc) {
       const bool in_b = (ngv & 1) != 0;
       if constexpr (G % 2 == 0) {
         if (in_b) {
@@ -1449,7 +1476,7 @@ __global__ __launch_bounds__(256 * WR, WR == 1 ? 2 : 1) void gemm_fused6_kernel(
       }
     }
   };
-  if constexpr (G % 2 == 0) {
+  if constexpr (G % 2 == 0 || SB) {
     for (int c = 0; c < Kc; ++c) chunk(c, w0, w1);
   } else {
     for (int c = 0; c < Kc; c += 2) {
@@ -1946,6 +1973,13 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
                          hipStream_t st) {
   const int g = (N + 255) / 256;
   const int wr = env_int("GCG_FUSED6_WR") == 2 ? 2 : 1;  // experiment: 2 row bands (8 waves)
+  if (env_int("GCG_FUSED6_WIDE") && g == 4) {  // experiment: 64 rows x 8 waves of 128 columns
+    hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
+                       dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale,
+                       scale_dev, loss_rows, correct_rows, row_w);
+    GCG_HIP_CHECK(hipGetLastError());
+    return GCG_OK;
+  }
   const dim3 grid(static_cast<unsigned>((M + 32 * wr - 1) / (32 * wr)));
 #define GCG_FUSED6_CASE(g_, wr_)                                                               \
   if (g == g_ && wr == wr_) {                                                                 \

@@ -175,9 +175,11 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
                                    (9, 4, 61)])
 def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
-    """gemm_fused6_kernel with two row bands per workgroup (GCG_FUSED6_WR=2, 8 waves) runs the
-    same products in the same order per element: bitwise the 4-wave kernel (gradient, loss,
-    hits, probabilities), rows past M included."""
+    """gemm_fused6_kernel with two row bands per workgroup (GCG_FUSED6_WR=2, 8 waves) and the wide
+    64-row tile (GCG_FUSED6_WIDE=1: 8 waves x 128 columns, one W register set, N > 768) run the
+    same products in the same order per element: the two-band kernel is bitwise the 4-wave one
+    (gradient, loss, hits, probabilities), rows past M included; the wide tile's row sums run
+    over 8 column waves (another association): within f32 rounding, the same hits."""
     monkeypatch.setenv("GCG_FUSED_MATH", "bf16x6")
     P, W, b = _rand((M, K), 51, 0.3), _rand((K, N), 52, 0.3), _rand((N,), 53)
     y = np.random.default_rng(54).integers(0, N, M).astype(np.int32)
@@ -185,8 +187,9 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     yt = torch.from_numpy(y).to(cuda)
     Wp = dense.Projection().fwd.get(Wt, False)
     outs = []
-    for wr in ("1", "2"):
-        monkeypatch.setenv("GCG_FUSED6_WR", wr)
+    for wr in ("1", "2", "wide"):
+        monkeypatch.setenv("GCG_FUSED6_WR", "1" if wr == "wide" else wr)
+        monkeypatch.setenv("GCG_FUSED6_WIDE", "1" if wr == "wide" else "0")
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
         dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
@@ -195,6 +198,13 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
         outs.append((G, loss, hits, probs))
     for a, ref in zip(outs[1], outs[0]):
         assert torch.equal(a, ref)
+    # the wide tile sums a row's exp over 8 column waves instead of 4: the same logits, another
+    # association of the row sum -- equal within f32 rounding, same hits
+    G2, l2, h2, p2 = outs[2]
+    assert torch.equal(h2, outs[0][2])
+    assert float((l2 - outs[0][1]).abs().max()) < 1e-5
+    assert float((G2 - outs[0][0]).abs().max()) < 1e-6 / M + 1e-9
+    assert float((p2 - outs[0][3]).abs().max()) < 1e-6
 
 
 def test_rows_softmax_xent_vs_float64(cuda):

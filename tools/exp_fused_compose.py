@@ -57,6 +57,13 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
         os.environ["GCG_FUSED6_WR"] = "2"
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
+        os.environ.pop("GCG_FUSED6_WR", None)
+
+    def fused6_wide():
+        os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        os.environ["GCG_FUSED6_WIDE"] = "1"
+        dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
+        os.environ.pop("GCG_FUSED6_WIDE", None)
 
     def compose():
         dense.gemm_nt(P, Wt, bias=b, out=G2, math="bf16x6")
@@ -75,7 +82,7 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     flops = 2.0 * T * K * C
     for rnd in range(3):
         for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose), ("fused_bf16x6", fused6),
-                         ("fused_bf16x6_8waves", fused6_wr2)):
+                         ("fused_bf16x6_8waves", fused6_wr2), ("fused_bf16x6_wide", fused6_wide)):
             ms = timeit(fn)
             rec.setdefault(name, []).append([round(ms, 3), round(flops / ms / 1e9, 1)])
     print(json.dumps(rec), flush=True)
