@@ -60,6 +60,33 @@ def test_bench_layout_bitwise(big):
     assert torch.equal(Yb, gs.spmm(A, Z, mode="ordered"))
 
 
+def test_class_width_layout_bitwise(big):
+    """The reference order's C-wide SpMM (mlpconv.py:90: H . (h . W2), C = 930 at World, 256 at
+    Twitter-US) on empty_dense's layout -- at World 960-float rows (the round-4 256-B rule) with
+    the masked last vector (930 % 4 != 0) and the default gather hint -- sampled rows and hubs
+    bitwise the oracle, with bias + rectify + gate on the same launch shape."""
+    cfg, H, A, Z = big
+    C = cfg.n_classes
+    g = torch.Generator(device=Z.device).manual_seed(9)
+    Zc = gs.empty_dense(cfg.n_nodes, C, Z.device).normal_(generator=g)
+    assert Zc.stride(0) == gs.row_stride(C) and (C != 930 or Zc.stride(0) == 960)
+    b = torch.randn(C, generator=g, device=Z.device)
+    gate = gs.empty_gate(cfg.n_nodes, C, Z.device)
+    Y = gs.spmm(A, Zc, bias=b, act="relu", gate=gate, mode="auto")
+    lens = np.diff(H.indptr)
+    rows = np.unique(np.concatenate([
+        np.random.default_rng(2).integers(0, cfg.n_nodes, 1500),
+        np.argsort(lens)[-100:],
+        [0, cfg.n_nodes - 1]]))
+    ref = O.spmm_f32(H, Zc.cpu().numpy(), rows=rows, bias=b.cpu().numpy(), act="relu")
+    rt = torch.as_tensor(rows, device=Y.device)
+    assert np.array_equal(Y[rt].cpu().numpy(), ref)
+    pre = O.spmm_f32(H, Zc.cpu().numpy(), rows=rows, bias=b.cpu().numpy())
+    want = np.where(pre > 0, 2, np.where(pre == 0, 1, 0)).astype(np.uint8)
+    assert np.array_equal(gate[rt].cpu().numpy(), want)
+    del Zc, Y, gate
+
+
 def test_fast_vs_ordered_and_checksums(big):
     cfg, H, A, Z = big
     Yo = gs.spmm(A, Z, mode="ordered")
