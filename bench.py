@@ -389,7 +389,8 @@ def dense_kernels_bench(reps: int, dev) -> dict:
            "note": "TFLOPs = useful f32 FLOP/s; frac against the f32 MFMA peak. gemm_nt (the "
                    "default, dense.NT_MATH) and the fused layer run bf16x6: six bf16 plane products per f32 "
                    "product on the bf16 matrix cores (error vs float64 <= the f32 kernel's, "
-                   "tests/test_dense_gpu.py); its frac = 6 x FLOP/s / the bf16 peak, "
+                   "tests/test_dense_gpu.py); the bf16x6 forms split the weight's planes into a "
+                   "workspace first, that launch inside the timed call; its frac = 6 x FLOP/s / the bf16 peak, "
                    "f32_equivalent_frac = FLOP/s / the f32 MFMA peak"}
     for name, fn in kernels.items():
         for _ in range(5):  # the first launches after a switch run while the clock ramps

@@ -76,6 +76,10 @@ SIGNATURES = {
     "gcg_gemm_nt_f32_bf16x6": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, C.c_int, _p,
                                          _i64, _p, _i64, _p]),
     "gcg_gemm_nt_bf16x6_workspace": (_i64, [_i64, _i64]),
+    "gcg_project_softmax_xent_bf16x6_workspace": (_i64, [_i64, _i64]),
+    "gcg_project_softmax_xent_weighted_ws_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64,
+                                                           _p, _p, C.c_float, _p, _p, _i64, _p,
+                                                           _p, _p, _p, _i64, _p]),
     "gcg_project_softmax_xent_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p,
                                                C.c_float, _p, _p, _i64, _p, _p, _p]),
     "gcg_softmax_xent_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, C.c_float, _p, _p, _i64, _p,

@@ -881,23 +881,38 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // LDS-DMA ring. The B image keeps gemm_nt_kernel's strided row order (row 16e + j of a 64-column
 // group holds column 4j + e), so the accumulator layout and the epilogue are the same.
 // ---------------------------------------------------------------------------------------
+// (element (n, k) at Bt + n * ldb + k * kstride: kstride = 1 for the NT weight Bt, ldw for the
+// fused layer's W read column-wise; planes for n in [N, n_out) are zero)
 __global__ __launch_bounds__(256) void split3_rows_kernel(int N, int K, int Kc,
                                                           const float* __restrict__ Bt, int64_t ldb,
-                                                          unsigned* __restrict__ out) {
+                                                          unsigned* __restrict__ out,
+                                                          int64_t kstride = 1, int n_out = 0) {
+  const int n_rows = n_out > N ? n_out : N;
   const int64_t i = static_cast<int64_t>(blockIdx.x) * 256 + threadIdx.x;  // (n, chunk, q)
-  if (i >= static_cast<int64_t>(N) * Kc * 4) return;
+  if (i >= static_cast<int64_t>(n_rows) * Kc * 4) return;
   const int q = static_cast<int>(i & 3);
   const int64_t nc = i >> 2;
   const int n = static_cast<int>(nc / Kc), c = static_cast<int>(nc % Kc);
-  const float* row = Bt + static_cast<int64_t>(n) * ldb;
+  const float* row = Bt + static_cast<int64_t>(n < N ? n : 0) * ldb;
   f8 x;
 #pragma unroll
   for (int w = 0; w < 8; ++w) {
     const int k = 32 * c + (w < 4 ? 4 * q + w : 16 + 4 * q + (w - 4));
-    x[w] = k < K ? row[k] : 0.f;
+    x[w] = (k < K && n < N) ? row[static_cast<int64_t>(k) * kstride] : 0.f;
   }
   bf8 h[3];
   split3(x, h[0], h[1], h[2]);
+  if (n_out > 0) {
+    // fused layer's layout [c][plane][n / 64][n % 4][(n % 64) / 4][q]: the 16 lanes j of one
+    // (column group, slot e, plane) read 16 x 64 contiguous bytes
+    const int gq = n >> 6, e = n & 3, jj = (n & 63) >> 2, ng = (n_rows + 63) >> 6;
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+      const int64_t pos = ((((static_cast<int64_t>(c) * 3 + p) * ng + gq) * 4 + e) * 16 + jj) * 16 + 4 * q;
+      *reinterpret_cast<u4v*>(out + pos) = __builtin_bit_cast(u4v, h[p]);
+    }
+    return;
+  }
   // [n][c][plane][32 bf16]: plane p's lane-q fragment is the 16 B at (nc * 3 + p) * 64 + 16 q
 #pragma unroll
   for (int p = 0; p < 3; ++p)
@@ -1285,13 +1300,13 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // are handled by the epilogue's straddle guard. All LDS (ring, row reductions, bias, labels,
 // row weights) is one array: a second __shared__ object makes hipcc drain the DMA queue.
 // ---------------------------------------------------------------------------------------
-template <int RT, int G, int WR = 1, int WC = 4, int SB = 0>
+template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0>
 __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused6_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
     const int32_t* __restrict__ labels, float scale, const float* __restrict__ scale_dev,
     float* __restrict__ loss_rows, float* __restrict__ correct_rows,
-    const float* __restrict__ row_w) {
+    const float* __restrict__ row_w, const unsigned* __restrict__ Wsplit = nullptr) {
   constexpr int EPI = 1, S = 2;
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   constexpr int STAGE = BM * 32;                 // A image floats per stage
@@ -1375,7 +1390,9 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   const int arow0 = wr * 16 * RT + j;
   f4 w0[8], w1[8];
   issue_a(0);
-  if (ngv > 0) load_w(0, 0, w0);
+  if constexpr (!FX) {
+    if (ngv > 0) load_w(0, 0, w0);
+  }
   auto group = [&](int c, int g, const bf8 (&ap)[RT][3], const f4 (&w)[8], f4 (&wn)[8]) {
     // prefetch the next group (or the next chunk's first) into the other set
     if (g + 1 < ngv) load_w(c, g + 1, wn);
@@ -1422,6 +1439,46 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       }
     }
   };
+  // FX = 1: W's bf16 planes pre-split into a workspace [BN][Kc][3][32] (split3_rows_kernel, zero
+  // past N): per group and chunk 12 loads of 16 B (4 column slots x 3 planes) and no split; the
+  // slot's column n = colw + 64 g + e + 4 j gives the scalar part (colw + 64 g + e) * Kc * 192
+  // layout (split3_rows_kernel, n_out = BN): [c][plane][BN / 64][e][j][q], 16 B per (j, q)
+  const int wlane = 64 * j + 16 * q;
+  constexpr int NG64 = BN / 64;
+  auto load_p = [&](int chunk, int g, f4 (&wp)[12]) {
+    // one chunk = 3 planes x NG64 groups x 4 slots x 1024 B
+    const auto rs = brsrc(Wsplit + chunk * 3 * NG64 * 1024, (Kc - chunk) * 3 * NG64 * 4096);
+    const int gq = colw / 64 + g;
+#pragma unroll
+    for (int e = 0; e < 4; ++e)
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        wp[3 * e + p] = __builtin_bit_cast(
+            f4, __builtin_amdgcn_raw_buffer_load_b128(rs, wlane, ((p * NG64 + gq) * 4 + e) * 1024, 0));
+  };
+  auto group_fx = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&wp)[12]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const bf8 b0 = __builtin_bit_cast(bf8, wp[3 * e]);
+      const bf8 b1 = __builtin_bit_cast(bf8, wp[3 * e + 1]);
+      const bf8 b2 = __builtin_bit_cast(bf8, wp[3 * e + 2]);
+      if (e == 3) {  // the set is consumed: the next group's planes fly during these MFMAs
+        if (g + 1 < ngv) load_p(c, g + 1, wp);
+        else if (c + 1 < Kc && ngv > 0) load_p(c + 1, 0, wp);
+      }
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        f4 cc = acc[t][g][e];
+        cc = mfma_bf(ap[t][2], b0, cc);
+        cc = mfma_bf(ap[t][1], b1, cc);
+        cc = mfma_bf(ap[t][0], b2, cc);
+        cc = mfma_bf(ap[t][1], b0, cc);
+        cc = mfma_bf(ap[t][0], b1, cc);
+        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+      }
+    }
+  };
+  f4 wpl[FX ? 12 : 1];
   // one chunk; wa holds its first group's W on entry. G even: the next chunk's first group
   // ends in wa again, G odd (G = 1, 3): in wb, so the loop alternates the sets (a wave whose
   // live-group count has the other parity -- it straddles N -- moves it)
@@ -1452,7 +1509,9 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
 #pragma unroll
     for (int g = 0; g < G; ++g) {
       if (g >= ngv) break;  // wave-uniform: groups wholly past N
-      if constexpr (SB) {
+      if constexpr (FX) {
+        group_fx(c, g, ap, wpl);
+      } else if constexpr (SB) {
         group_sb(c, g, ap, wa);
       } else if (g % 2 == 0) {
         group(c, g, ap, wa, wb);
@@ -1461,7 +1520,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       }
     }
     // the last live group (ngv - 1) prefetched the next chunk's first into wb when ngv is odd
-    if (!SB && ngv > 0 && c + 1 < Kc) {
+    if (!SB && !FX && ngv > 0 && c + 1 < Kc) {
       const bool in_b = (ngv & 1) != 0;
       if constexpr (G % 2 == 0) {
         if (in_b) {
@@ -1476,7 +1535,10 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       }
     }
   };
-  if constexpr (G % 2 == 0 || SB) {
+  if constexpr (FX) {
+    if (ngv > 0) load_p(0, 0, wpl);
+  }
+  if constexpr (G % 2 == 0 || SB || FX) {
     for (int c = 0; c < Kc; ++c) chunk(c, w0, w1);
   } else {
     for (int c = 0; c < Kc; c += 2) {
@@ -1970,8 +2032,34 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
                          int64_t ldb, const float* bias, float* C, int64_t ldc,
                          const int32_t* labels, float scale, const float* scale_dev,
                          float* loss_rows, float* correct_rows, const float* row_w,
-                         hipStream_t st) {
+                         hipStream_t st, void* ws = nullptr) {
   const int g = (N + 255) / 256;
+  if (ws != nullptr) {  // the weight's planes pre-split (FX = 1) for the tile's BN columns
+    const int Kc = (K + 31) / 32;
+    const bool wide = env_int("GCG_FUSED6_FX_WIDE") && g == 4;
+    const int bn = wide ? 1024 : 256 * g;
+    const int64_t threads = int64_t{bn} * Kc * 4;
+    hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)),
+                       dim3(256), 0, st, N, K, Kc, B, int64_t{1}, static_cast<unsigned*>(ws), ldb,
+                       bn);
+    GCG_HIP_CHECK(hipGetLastError());
+    const auto* wsp = static_cast<const unsigned*>(ws);
+    if (wide) {
+      hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 0, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
+                         dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels,
+                         scale, scale_dev, loss_rows, correct_rows, row_w, wsp);
+    } else {
+      const dim3 grid(static_cast<unsigned>((M + 31) / 32));
+      switch (g) {
+        case 1: hipLaunchKernelGGL((gemm_fused6_kernel<2, 1, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 2: hipLaunchKernelGGL((gemm_fused6_kernel<2, 2, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 3: hipLaunchKernelGGL((gemm_fused6_kernel<2, 3, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        default: hipLaunchKernelGGL((gemm_fused6_kernel<2, 4, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+      }
+    }
+    GCG_HIP_CHECK(hipGetLastError());
+    return GCG_OK;
+  }
   const int wr = env_int("GCG_FUSED6_WR") == 2 ? 2 : 1;  // experiment: 2 row bands (8 waves)
   if (env_int("GCG_FUSED6_WIDE") && g == 4) {  // experiment: 64 rows x 8 waves of 128 columns
     hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
@@ -2006,7 +2094,7 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
                        const float* bias, int act, float* C, int64_t ldc,
                        const int32_t* labels, float scale, const float* scale_dev,
                        float* loss_rows, float* correct_rows, const float* row_w,
-                       gcg_stream_t stream) {
+                       gcg_stream_t stream, void* ws = nullptr) {
   if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
                 static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
@@ -2038,7 +2126,7 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
   auto st = static_cast<hipStream_t>(stream);
   if (fused && fused_bf16x6())
     return launch_fused6(M, int(N), int(K), A, lda, B, ldb, bias, C, ldc, labels, scale,
-                         scale_dev, loss_rows, correct_rows, row_w, st);
+                         scale_dev, loss_rows, correct_rows, row_w, st, ws);
   if (fused)
     return launch_gemm<1>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
                           labels, scale, scale_dev, loss_rows, correct_rows, row_w);
@@ -2358,6 +2446,28 @@ gcg_status gcg_project_softmax_xent_weighted_f32(int64_t M, int64_t N, int64_t K
   return gemm_common("gcg_project_softmax_xent_weighted_f32", true, M, N, K, A, lda, W, ldw,
                      bias, GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows,
                      correct_rows, row_weight, stream);
+}
+
+int64_t gcg_project_softmax_xent_bf16x6_workspace(int64_t N, int64_t K) {
+  if (N <= 0 || N > 1024 || K <= 0) return 0;
+  return int64_t{1024} * ((K + 31) / 32) * 192;
+}
+
+gcg_status gcg_project_softmax_xent_weighted_ws_f32(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
+    const float* bias, const int32_t* labels, float scale, const float* scale_dev, float* out,
+    int64_t ldo, float* loss_rows, float* correct_rows, const float* row_weight, void* ws,
+    int64_t ws_bytes, gcg_stream_t stream) {
+  const char* fn = "gcg_project_softmax_xent_weighted_ws_f32";
+  if (ws != nullptr) {
+    if (ws_bytes < gcg_project_softmax_xent_bf16x6_workspace(N, K))
+      return fail(GCG_ERR_INVALID_ARG, "%s: workspace %lld B too small", fn,
+                  static_cast<long long>(ws_bytes));
+    if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
+    if (int64_t{1024} * ((K + 31) / 32) * 192 > INT32_MAX) ws = nullptr;  // 32-bit offsets
+  }
+  return gemm_common(fn, true, M, N, K, A, lda, W, ldw, bias, GCG_ACT_NONE, out, ldo, labels,
+                     scale, scale_dev, loss_rows, correct_rows, row_weight, stream, ws);
 }
 
 gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,

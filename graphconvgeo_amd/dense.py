@@ -416,6 +416,13 @@ def _row_weight(w: Optional[torch.Tensor], M: int) -> Optional[torch.Tensor]:
     return w.detach().to(torch.float32).contiguous()
 
 
+# fused layer (bf16x6): W's planes pre-split once per call into a workspace laid out for
+# coalesced loads (FX = 1) instead of split in every workgroup's registers -- World 840k x 300 x
+# 930 136.5-136.8 vs 123.1-123.6 TFLOP/s f32-equivalent, bitwise the same products
+# (tools/exp_fused_compose.py, test_fused6_row_bands_bitwise)
+FUSED_PRESPLIT = True
+
+
 def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weight=None):
     P = _aligned_operand(P, "P")
     M, K = P.shape
@@ -429,11 +436,15 @@ def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weig
         b = b.detach().contiguous()
     if M == 0:
         return
+    ws, nb = None, 0
+    if FUSED_PRESPLIT:  # the weight's bf16 planes split once per call into a workspace
+        nb = int(load().gcg_project_softmax_xent_bf16x6_workspace(N, K))
+        ws = torch.empty(nb, dtype=torch.uint8, device=P.device)
     with torch.cuda.device(P.device):
-        call("gcg_project_softmax_xent_weighted_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp),
+        call("gcg_project_softmax_xent_weighted_ws_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp),
              Wp.stride(0), _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
              _ld(out) if out is not None else 0, _ptr(loss_rows), _ptr(correct),
-             _ptr(row_weight), _stream_handle(P.device))
+             _ptr(row_weight), _ptr(ws), nb, _stream_handle(P.device))
 
 
 class _ProjectXent(torch.autograd.Function):

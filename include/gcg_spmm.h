@@ -398,6 +398,23 @@ gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const f
                                         float* correct_rows /*nullable*/, gcg_stream_t stream);
 
 /*
+ * gcg_project_softmax_xent_weighted_ws_f32: gcg_project_softmax_xent_weighted_f32 with a
+ * workspace (bytes: gcg_project_softmax_xent_bf16x6_workspace(N, K), 16-B aligned): on the bf16
+ * matrix cores the weight's three bf16 planes are split once per call into it (a small kernel on
+ * the same stream) instead of in every workgroup's registers -- bitwise the same results, ~10 %
+ * faster at Twitter-World's shapes; the package's default path (graphconvgeo_amd/dense.py).
+ * ws == NULL or GCG_FUSED_MATH=f32: the plain entry's kernels; a workspace smaller than
+ * gcg_project_softmax_xent_bf16x6_workspace(N, K): GCG_ERR_INVALID_ARG.
+ */
+int64_t gcg_project_softmax_xent_bf16x6_workspace(int64_t N, int64_t K);
+gcg_status gcg_project_softmax_xent_weighted_ws_f32(
+    int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
+    const float* bias /*nullable*/, const int32_t* labels /*nullable*/, float scale,
+    const float* scale_dev /*nullable*/, float* out /*nullable*/, int64_t ldo, float* loss_rows,
+    float* correct_rows /*nullable*/, const float* row_weight /*nullable*/, void* ws /*nullable*/,
+    int64_t ws_bytes, gcg_stream_t stream);
+
+/*
  * The same row epilogue for logits that already exist (the reference order, where the
  * logits are the H SpMM's output rows, mlpconv.py:90-94): one wave per row, N <= 4096,
  * out may alias logits; out == NULL computes loss_rows / correct_rows only (the forward

@@ -175,36 +175,43 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
                                    (9, 4, 61)])
 def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
-    """gemm_fused6_kernel with two row bands per workgroup (GCG_FUSED6_WR=2, 8 waves) and the wide
-    64-row tile (GCG_FUSED6_WIDE=1: 8 waves x 128 columns, one W register set, N > 768) run the
-    same products in the same order per element: the two-band kernel is bitwise the 4-wave one
-    (gradient, loss, hits, probabilities), rows past M included; the wide tile's row sums run
-    over 8 column waves (another association): within f32 rounding, the same hits."""
+    """gemm_fused6_kernel's forms: the weight split in registers (dense.FUSED_PRESPLIT off) with
+    one row band (4 waves), two row bands (GCG_FUSED6_WR=2, 8 waves) and the wide 64-row tile
+    (GCG_FUSED6_WIDE=1: 8 waves x 128 columns, one W register set, N > 768); the weight's planes
+    pre-split into a workspace (the default) with the 4-wave and the wide tile
+    (GCG_FUSED6_FX_WIDE=1). The same products in the same order per element: the 4-wave forms
+    and the two-band form are bitwise equal (gradient, loss, hits, probabilities), rows past M
+    included; the wide tiles' row sums run over 8 column waves (another association): within
+    f32 rounding, the same hits."""
     monkeypatch.setenv("GCG_FUSED_MATH", "bf16x6")
     P, W, b = _rand((M, K), 51, 0.3), _rand((K, N), 52, 0.3), _rand((N,), 53)
     y = np.random.default_rng(54).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
     yt = torch.from_numpy(y).to(cuda)
     Wp = dense.Projection().fwd.get(Wt, False)
-    outs = []
-    for wr in ("1", "2", "wide"):
-        monkeypatch.setenv("GCG_FUSED6_WR", "1" if wr == "wide" else wr)
-        monkeypatch.setenv("GCG_FUSED6_WIDE", "1" if wr == "wide" else "0")
+
+    def run(presplit, wr="1", wide="0", fx_wide="0"):
+        monkeypatch.setattr(dense, "FUSED_PRESPLIT", presplit)
+        monkeypatch.setenv("GCG_FUSED6_WR", wr)
+        monkeypatch.setenv("GCG_FUSED6_WIDE", wide)
+        monkeypatch.setenv("GCG_FUSED6_FX_WIDE", fx_wide)
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
         dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
         probs = empty_dense(M, N, cuda)
         dense._fused(Pt, Wp, bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None)
-        outs.append((G, loss, hits, probs))
-    for a, ref in zip(outs[1], outs[0]):
-        assert torch.equal(a, ref)
-    # the wide tile sums a row's exp over 8 column waves instead of 4: the same logits, another
-    # association of the row sum -- equal within f32 rounding, same hits
-    G2, l2, h2, p2 = outs[2]
-    assert torch.equal(h2, outs[0][2])
-    assert float((l2 - outs[0][1]).abs().max()) < 1e-5
-    assert float((G2 - outs[0][0]).abs().max()) < 1e-6 / M + 1e-9
-    assert float((p2 - outs[0][3]).abs().max()) < 1e-6
+        return G, loss, hits, probs
+
+    ref = run(False)
+    for o in (run(False, wr="2"), run(True)):
+        for a, r in zip(o, ref):
+            assert torch.equal(a, r)
+    for o in (run(False, wide="1"), run(True, fx_wide="1")):
+        G2, l2, h2, p2 = o
+        assert torch.equal(h2, ref[2])
+        assert float((l2 - ref[1]).abs().max()) < 1e-5
+        assert float((G2 - ref[0]).abs().max()) < 1e-6 / M + 1e-9
+        assert float((p2 - ref[3]).abs().max()) < 1e-6
 
 
 def test_rows_softmax_xent_vs_float64(cuda):

@@ -51,17 +51,34 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     def fused6():
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
         os.environ.pop("GCG_FUSED6_WR", None)
+        dense.FUSED_PRESPLIT = False
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
 
     def fused6_wr2():
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
         os.environ["GCG_FUSED6_WR"] = "2"
+        dense.FUSED_PRESPLIT = False
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
         os.environ.pop("GCG_FUSED6_WR", None)
+
+    def fused6_fx():
+        os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        dense.FUSED_PRESPLIT = True
+        dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
+        dense.FUSED_PRESPLIT = False
+
+    def fused6_fx_wide():
+        os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        os.environ["GCG_FUSED6_FX_WIDE"] = "1"
+        dense.FUSED_PRESPLIT = True
+        dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
+        dense.FUSED_PRESPLIT = False
+        os.environ.pop("GCG_FUSED6_FX_WIDE", None)
 
     def fused6_wide():
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
         os.environ["GCG_FUSED6_WIDE"] = "1"
+        dense.FUSED_PRESPLIT = False
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
         os.environ.pop("GCG_FUSED6_WIDE", None)
 
@@ -74,6 +91,11 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     torch.cuda.synchronize()
     rec = {"shape": f"{T}x{K}x{C}", "G_maxdiff": float((G1 - G2).abs().max()),
            "loss_maxdiff": float((l1 - l2).abs().max()), "hits_diff": float((h1 - h2).abs().sum())}
+    fused6_fx()
+    torch.cuda.synchronize()
+    rec.update(G_maxdiff_presplit=float((G1 - G2).abs().max()),
+               loss_maxdiff_presplit=float((l1 - l2).abs().max()),
+               hits_diff_presplit=float((h1 - h2).abs().sum()))
     fused6()
     torch.cuda.synchronize()
     rec.update(G_maxdiff_fused6=float((G1 - G2).abs().max()),
@@ -82,7 +104,8 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     flops = 2.0 * T * K * C
     for rnd in range(3):
         for name, fn in (("fused_f32", fused), ("compose_bf16x6", compose), ("fused_bf16x6", fused6),
-                         ("fused_bf16x6_8waves", fused6_wr2), ("fused_bf16x6_wide", fused6_wide)):
+                         ("fused_bf16x6_8waves", fused6_wr2), ("fused_bf16x6_wide", fused6_wide),
+                         ("fused_bf16x6_presplit", fused6_fx), ("fused_bf16x6_presplit_wide", fused6_fx_wide)):
             ms = timeit(fn)
             rec.setdefault(name, []).append([round(ms, 3), round(flops / ms / 1e9, 1)])
     print(json.dumps(rec), flush=True)
