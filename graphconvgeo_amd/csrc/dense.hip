@@ -1445,27 +1445,29 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   // layout (split3_rows_kernel, n_out = BN): [c][plane][BN / 64][e][j][q], 16 B per (j, q)
   const int wlane = 64 * j + 16 * q;
   constexpr int NG64 = BN / 64;
-  auto load_p = [&](int chunk, int g, f4 (&wp)[12]) {
+  // the 3 planes of slot e (columns colw + 64 g + e + 4 j) of one chunk and group
+  auto load_slot = [&](int chunk, int g, int e, f4 (&wp)[12]) {
     // one chunk = 3 planes x NG64 groups x 4 slots x 1024 B
     const auto rs = brsrc(Wsplit + chunk * 3 * NG64 * 1024, (Kc - chunk) * 3 * NG64 * 4096);
     const int gq = colw / 64 + g;
 #pragma unroll
-    for (int e = 0; e < 4; ++e)
-#pragma unroll
-      for (int p = 0; p < 3; ++p)
-        wp[3 * e + p] = __builtin_bit_cast(
-            f4, __builtin_amdgcn_raw_buffer_load_b128(rs, wlane, ((p * NG64 + gq) * 4 + e) * 1024, 0));
+    for (int p = 0; p < 3; ++p)
+      wp[3 * e + p] = __builtin_bit_cast(
+          f4, __builtin_amdgcn_raw_buffer_load_b128(rs, wlane, ((p * NG64 + gq) * 4 + e) * 1024, 0));
   };
+  auto load_p = [&](int chunk, int g, f4 (&wp)[12]) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) load_slot(chunk, g, e, wp);
+  };
+  // one register set, refilled slot by slot: once slot e's MFMAs are issued its registers take
+  // the next group's (or the next chunk's first group's) slot e, so each load has three slots
+  // of MFMAs (and the other waves' work) to land in
   auto group_fx = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&wp)[12]) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const bf8 b0 = __builtin_bit_cast(bf8, wp[3 * e]);
       const bf8 b1 = __builtin_bit_cast(bf8, wp[3 * e + 1]);
       const bf8 b2 = __builtin_bit_cast(bf8, wp[3 * e + 2]);
-      if (e == 3) {  // the set is consumed: the next group's planes fly during these MFMAs
-        if (g + 1 < ngv) load_p(c, g + 1, wp);
-        else if (c + 1 < Kc && ngv > 0) load_p(c + 1, 0, wp);
-      }
 #pragma unroll
       for (int t = 0; t < RT; ++t) {
         f4 cc = acc[t][g][e];
@@ -1476,6 +1478,8 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
         cc = mfma_bf(ap[t][0], b1, cc);
         acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
       }
+      if (g + 1 < ngv) load_slot(c, g + 1, e, wp);
+      else if (c + 1 < Kc && ngv > 0) load_slot(c + 1, 0, e, wp);
     }
   };
   f4 wpl[FX ? 12 : 1];
@@ -1483,7 +1487,10 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   // ends in wa again, G odd (G = 1, 3): in wb, so the loop alternates the sets (a wave whose
   // live-group count has the other parity -- it straddles N -- moves it)
   auto chunk = [&](int c, f4 (&wa)[8], f4 (&wb)[8]) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // A(c) landed (and W's prefetch)
+    // A(c) landed. FX with live groups: the last 12 loads issued (this chunk's first group of
+    // planes, prefetched by the previous chunk's last group or the prologue) may still fly
+    if (FX && ngv > 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (and W's prefetch)
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (c + 1 < Kc) issue_a(c + 1);
@@ -2036,7 +2043,9 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
   const int g = (N + 255) / 256;
   if (ws != nullptr) {  // the weight's planes pre-split (FX = 1) for the tile's BN columns
     const int Kc = (K + 31) / 32;
-    const bool wide = env_int("GCG_FUSED6_FX_WIDE") && g == 4;
+    // N > 768: 64 rows x 8 waves of 128 columns (the weight's planes read once per 64 rows,
+    // half the 32-row form's L2 reads); GCG_FUSED6_FX_NARROW=1 keeps the 32-row 4-wave form
+    const bool wide = g == 4 && !env_int("GCG_FUSED6_FX_NARROW");
     const int bn = wide ? 1024 : 256 * g;
     const int64_t threads = int64_t{bn} * Kc * 4;
     hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)),

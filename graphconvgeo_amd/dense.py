@@ -417,8 +417,8 @@ def _row_weight(w: Optional[torch.Tensor], M: int) -> Optional[torch.Tensor]:
 
 
 # fused layer (bf16x6): W's planes pre-split once per call into a workspace laid out for
-# coalesced loads (FX = 1) instead of split in every workgroup's registers -- World 840k x 300 x
-# 930 136.5-136.8 vs 123.1-123.6 TFLOP/s f32-equivalent, bitwise the same products
+# coalesced loads (FX = 1) instead of split in every workgroup's registers; at N > 768 on a
+# 64-row tile -- World 840k x 300 x 930 140-147.5 vs 121-128 TFLOP/s f32-equivalent
 # (tools/exp_fused_compose.py, test_fused6_row_bands_bitwise)
 FUSED_PRESPLIT = True
 

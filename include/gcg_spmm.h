@@ -401,8 +401,10 @@ gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const f
  * gcg_project_softmax_xent_weighted_ws_f32: gcg_project_softmax_xent_weighted_f32 with a
  * workspace (bytes: gcg_project_softmax_xent_bf16x6_workspace(N, K), 16-B aligned): on the bf16
  * matrix cores the weight's three bf16 planes are split once per call into it (a small kernel on
- * the same stream) instead of in every workgroup's registers -- bitwise the same results, ~10 %
- * faster at Twitter-World's shapes; the package's default path (graphconvgeo_amd/dense.py).
+ * the same stream) instead of in every workgroup's registers, and at N > 768 on 64-row tiles
+ * (8 waves; row sums over 8 column waves: within f32 rounding of the plain entry, the same
+ * hits); 10-20 % faster at Twitter-World's shapes; the package's default path
+ * (graphconvgeo_amd/dense.py). GCG_FUSED6_FX_NARROW=1: 32-row tiles, bitwise the plain entry.
  * ws == NULL or GCG_FUSED_MATH=f32: the plain entry's kernels; a workspace smaller than
  * gcg_project_softmax_xent_bf16x6_workspace(N, K): GCG_ERR_INVALID_ARG.
  */

@@ -178,8 +178,8 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     """gemm_fused6_kernel's forms: the weight split in registers (dense.FUSED_PRESPLIT off) with
     one row band (4 waves), two row bands (GCG_FUSED6_WR=2, 8 waves) and the wide 64-row tile
     (GCG_FUSED6_WIDE=1: 8 waves x 128 columns, one W register set, N > 768); the weight's planes
-    pre-split into a workspace (the default) with the 4-wave and the wide tile
-    (GCG_FUSED6_FX_WIDE=1). The same products in the same order per element: the 4-wave forms
+    pre-split into a workspace (the default) with the wide tile (the default at N > 768) and the
+    4-wave tile (GCG_FUSED6_FX_NARROW=1). The same products in the same order per element: the 4-wave forms
     and the two-band form are bitwise equal (gradient, loss, hits, probabilities), rows past M
     included; the wide tiles' row sums run over 8 column waves (another association): within
     f32 rounding, the same hits."""
@@ -190,11 +190,11 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     yt = torch.from_numpy(y).to(cuda)
     Wp = dense.Projection().fwd.get(Wt, False)
 
-    def run(presplit, wr="1", wide="0", fx_wide="0"):
+    def run(presplit, wr="1", wide="0", fx_narrow="0"):
         monkeypatch.setattr(dense, "FUSED_PRESPLIT", presplit)
         monkeypatch.setenv("GCG_FUSED6_WR", wr)
         monkeypatch.setenv("GCG_FUSED6_WIDE", wide)
-        monkeypatch.setenv("GCG_FUSED6_FX_WIDE", fx_wide)
+        monkeypatch.setenv("GCG_FUSED6_FX_NARROW", fx_narrow)
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
         dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
@@ -203,10 +203,10 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
         return G, loss, hits, probs
 
     ref = run(False)
-    for o in (run(False, wr="2"), run(True)):
+    for o in (run(False, wr="2"), run(True, fx_narrow="1")):
         for a, r in zip(o, ref):
             assert torch.equal(a, r)
-    for o in (run(False, wide="1"), run(True, fx_wide="1")):
+    for o in (run(False, wide="1"), run(True)):
         G2, l2, h2, p2 = o
         assert torch.equal(h2, ref[2])
         assert float((l2 - ref[1]).abs().max()) < 1e-5

@@ -61,19 +61,19 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
         os.environ.pop("GCG_FUSED6_WR", None)
 
-    def fused6_fx():
+    def fused6_fx():  # pre-split planes, the 32-row 4-wave tile
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
+        os.environ["GCG_FUSED6_FX_NARROW"] = "1"
         dense.FUSED_PRESPLIT = True
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
         dense.FUSED_PRESPLIT = False
+        os.environ.pop("GCG_FUSED6_FX_NARROW", None)
 
-    def fused6_fx_wide():
+    def fused6_fx_wide():  # pre-split planes, the default tile (64 rows x 8 waves at N > 768)
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
-        os.environ["GCG_FUSED6_FX_WIDE"] = "1"
         dense.FUSED_PRESPLIT = True
         dense._fused(P, Wp, b, y, 1.0 / T, None, G2, l2, h2)
         dense.FUSED_PRESPLIT = False
-        os.environ.pop("GCG_FUSED6_FX_WIDE", None)
 
     def fused6_wide():
         os.environ["GCG_FUSED_MATH"] = "bf16x6"
@@ -96,6 +96,11 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     rec.update(G_maxdiff_presplit=float((G1 - G2).abs().max()),
                loss_maxdiff_presplit=float((l1 - l2).abs().max()),
                hits_diff_presplit=float((h1 - h2).abs().sum()))
+    fused6_fx_wide()
+    torch.cuda.synchronize()
+    rec.update(G_maxdiff_presplit_wide=float((G1 - G2).abs().max()),
+               loss_maxdiff_presplit_wide=float((l1 - l2).abs().max()),
+               hits_diff_presplit_wide=float((h1 - h2).abs().sum()))
     fused6()
     torch.cuda.synchronize()
     rec.update(G_maxdiff_fused6=float((G1 - G2).abs().max()),
