@@ -120,6 +120,37 @@ def test_fused_softmax_xent_vs_float64(cuda, M, K, N, math, monkeypatch):
     assert torch.equal(loss, loss2)
 
 
+@pytest.mark.parametrize("N", [129, 930])
+@pytest.mark.parametrize("math", ["bf16x6", "f32"])
+def test_fused_labels_outside_classes(cuda, N, math, monkeypatch):
+    """A label outside [0, N) (-1, N, N + 7; the C-ABI does not check labels on the host): that
+    row's loss is NaN, its hit 0, and its gradient row the probabilities times scale (no onehot
+    subtracted); every other row as with valid labels. Both maths, the 64-row tile at N = 930."""
+    monkeypatch.setenv("GCG_FUSED_MATH", math)
+    M, K = 70, 33
+    P, W, b = _rand((M, K), 61, 0.3), _rand((K, N), 62, 0.3), _rand((N,), 63)
+    y = np.random.default_rng(64).integers(0, N, M).astype(np.int32)
+    bad = np.array([3, 17, 40, 69])
+    y[bad] = [-1, N, N + 7, -5]
+    ok = np.ones(M, bool)
+    ok[bad] = False
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    G = empty_dense(M, N, cuda)
+    loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+    dense._fused(Pt, dense.Projection().fwd.get(Wt, False), bt, yt, 1.0 / M, None, G, loss, hits)
+    logits64 = P.astype(np.float64) @ W.astype(np.float64) + b
+    P64, loss64, hits64, G64 = O.softmax_xent_f64(logits64, np.where(ok, y, 0))
+    lo, hi, Gc = loss.cpu().numpy(), hits.cpu().numpy(), G.cpu().numpy()
+    assert np.isnan(lo[bad]).all() and (hi[bad] == 0).all()
+    assert np.abs(Gc[bad] - P64[bad] / M).max() < 1e-5 / M + 1e-7
+    assert np.abs(lo[ok] - loss64[ok]).max() < 1e-5
+    assert np.abs(Gc[ok] - G64[ok]).max() < 1e-5 / M + 1e-7
+    srt = np.sort(logits64, axis=1)
+    clear = ok & ((srt[:, -1] - srt[:, -2]) > 1e-4)
+    assert np.array_equal(hi[clear], hits64[clear])
+
+
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (20, 3, 61), (9, 4, 522),
                                    (40, 50, 300), (70, 300, 600)])
 @pytest.mark.parametrize("math", ["bf16x6", "f32"])
@@ -173,7 +204,7 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
 
 
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
-                                   (9, 4, 61)])
+                                   (9, 4, 61), (5, 7, 801), (128, 64, 1021)])
 def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     """gemm_fused6_kernel's forms: the weight split in registers (dense.FUSED_PRESPLIT off) with
     one row band (4 waves), two row bands (GCG_FUSED6_WR=2, 8 waves) and the wide 64-row tile
