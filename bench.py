@@ -813,7 +813,6 @@ def main():
             alt = {"error": f"{type(exc).__name__}: {exc}"[:500]}
 
     value = B / (ms * 1e-3) / 1e9
-    value = B / (ms * 1e-3) / 1e9
     rec = {
         "metric": "GCN SpMM fwd GB/s (achieved HBM) + edges/s, Twitter-World graph, 1/2/4/8 GPU",
         "value": round(value), "unit": "GB/s",
