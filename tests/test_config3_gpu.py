@@ -72,7 +72,7 @@ def test_twitter_us_fwd_bwd(cuda, us, order):
     y = torch.as_tensor(us["Y"][us["train"]].astype(np.int32), device=cuda)
     loss, _acc = clf._loss_acc(rows, y)
     loss.backward()
-    assert abs(float(loss) - us["loss64"]) <= 1e-5 * max(1.0, abs(us["loss64"]))
+    assert abs(float(loss.detach()) - us["loss64"]) <= 1e-5 * max(1.0, abs(us["loss64"]))
     for p, k in zip(clf.params, ("W1", "b1", "W2", "b2")):
         got = p.grad.detach().cpu().numpy().astype(np.float64)
         ref = us["g64"][k]

@@ -57,3 +57,42 @@ def test_column_sum_matches_float64(M, K, ld):
     np.testing.assert_allclose(s.cpu().numpy(), ref, rtol=0,
                                atol=2e-6 * np.abs(X[:, :K]).sum(0).max() + 1e-7)
     assert torch.equal(s, gs.column_sum(Xd))  # deterministic
+
+
+def _colsum_in_kernel_order(X):
+    """numpy float32 restatement of the kernels' summation order (csr_ops.hip): blocks of rpb
+    rows, wave w of a block adding rows w, w + 4, ... in order, the 4 waves combined
+    ((0 + 1) + 2) + 3; then 16 streams over the block partials (stream s: blocks s, s + 16, ...)
+    added 0..15 in order."""
+    M, K = X.shape
+    r = -(-M // 1024)
+    rpb = max(512, (r + 3) // 4 * 4)
+    nb = -(-M // rpb)
+    part = np.zeros((nb, K), np.float32)
+    for b in range(nb):
+        r0, r1 = b * rpb, min(M, (b + 1) * rpb)
+        acc = np.zeros((4, K), np.float32)
+        for i in range(r0, r1):
+            acc[(i - r0) % 4] += X[i]
+        part[b] = ((acc[0] + acc[1]) + acc[2]) + acc[3]
+    s = np.zeros((16, K), np.float32)
+    for b in range(nb):
+        s[b % 16] += part[b]
+    t = s[0].copy()
+    for i in range(1, 16):
+        t += s[i]
+    return t
+
+
+@pytest.mark.parametrize("M,K,ld", [(20_000, 930, 960), (10_247, 300, 304), (9_000, 301, 301)])
+def test_column_sums_follow_the_documented_order(M, K, ld):
+    """Bitwise: the bias gradients are the fixed-order sums the kernels document (so a change
+    of the finishing kernel's workgroup shape cannot move a bit)."""
+    rng = np.random.default_rng(K)
+    X = rng.standard_normal((M, ld)).astype(np.float32)
+    Y = np.maximum(rng.standard_normal((M, ld)), 0).astype(np.float32)
+    Xd = torch.from_numpy(X).cuda()[:, :K]
+    np.testing.assert_array_equal(gs.column_sum(Xd).cpu().numpy(), _colsum_in_kernel_order(X[:, :K]))
+    _, db = gs.relu_backward(Xd, torch.from_numpy(Y).cuda()[:, :K])
+    masked = np.where(Y[:, :K] > 0, X[:, :K], np.float32(0))
+    np.testing.assert_array_equal(db.cpu().numpy(), _colsum_in_kernel_order(masked))

@@ -11,7 +11,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from graphconvgeo_amd import sparse as gs  # noqa: E402
 
 dev = torch.device("cuda:0")
-for M, K in ((1_400_000, 300), (450_000, 300), (840_000, 930)):
+for M, K in ((1_400_000, 300), (450_000, 300), (840_000, 930), (530_956, 930)):
     g = gs.empty_dense(M, K, dev).normal_()
     gate = gs.empty_gate(M, K, dev)
     gate.copy_(torch.randint(0, 3, (M, K), device=dev, dtype=torch.uint8))
