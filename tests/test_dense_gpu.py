@@ -289,7 +289,7 @@ def test_rows_xent_autograd_and_matmul_autograd(cuda):
     (0.5 * loss).backward()
     _, loss64, _, G64 = O.softmax_xent_f64(A.astype(np.float64) @ W + b, y)
     G64 *= 0.5
-    assert abs(float(loss) - loss64.mean()) < 1e-5
+    assert abs(float(loss.detach()) - loss64.mean()) < 1e-5
     assert np.abs(At.grad.cpu().numpy() - G64 @ W.T.astype(np.float64)).max() < 1e-6
     assert np.abs(Wt.grad.cpu().numpy() - A.T.astype(np.float64) @ G64).max() < 1e-6
     assert np.abs(bt.grad.cpu().numpy() - G64.sum(0)).max() < 1e-6
