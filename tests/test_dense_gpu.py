@@ -531,8 +531,8 @@ def test_l1l2_penalty_vs_float64(cuda):
     pen = dense.l1l2_penalty(Ws, coefs)
     ref = sum(l1 * np.abs(W.astype(np.float64)).sum() + l2 * (W.astype(np.float64) ** 2).sum()
               for W, (l1, l2) in zip((W2, W1), coefs))
-    assert abs(float(pen) - ref) <= 1e-6 * ref
-    assert float(dense.l1l2_penalty(Ws, coefs)) == float(pen)
+    assert abs(float(pen.detach()) - ref) <= 1e-6 * ref
+    assert float(dense.l1l2_penalty(Ws, coefs).detach()) == float(pen.detach())
     (pen * 3.0).backward()
     for W, Wt, (l1, l2) in zip((W2, W1), Ws, coefs):
         g64 = 3.0 * (l1 * np.sign(W.astype(np.float64)) + 2 * l2 * W.astype(np.float64))
