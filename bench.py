@@ -215,15 +215,34 @@ def _read_counter(d: str, counter: str, kernel: str = PMC_KERNEL):
     return [per[k] for k in sorted(per)]
 
 
-def live_traffic(H, K: int, mode: str, timeout_s: int = 240) -> dict:
-    """HBM-side bytes of the bench's own SpMM launch, measured in this run: tools/pmc_probe.py
-    (same graph, layout, mode and gather hint) under `rocprofv3 --pmc FETCH_SIZE` and
-    `--pmc WRITE_SIZE`, one child process per pass (run before this process touches the GPU),
-    each bounded by `timeout -s KILL`. Per launch: 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes;
-    the gfx950 correction of MI355X_MICROARCH.md:298), the mean over the launches after the
-    plan-building one. These are L2->fabric bytes: reads the Infinity Cache serves are counted
-    too (no gfx950 TCC counter separates them), so they bound the DRAM bytes from
-    above."""
+def _read_kernel_trace(d: str, kernel: str = PMC_KERNEL):
+    """Per-dispatch durations (ns, dispatch order) of `kernel` from a rocprofv3 kernel trace."""
+    import csv
+    import glob
+    rows = []
+    for fn in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        with open(fn) as fh:
+            for row in csv.DictReader(fh):
+                if kernel in row["Kernel_Name"]:
+                    rows.append((int(row.get("Dispatch_Id", 0) or 0),
+                                 int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    return [ns for _d, ns in sorted(rows)]
+
+
+def live_traffic(H, K: int, mode: str, timeout_s: int = 240, keep_dir: str = "",
+                 tag: str = "headline", launches: int = 20) -> dict:
+    """Measured in this run, before this process touches the GPU, by child processes that replay
+    the bench's own SpMM launch (tools/pmc_probe.py: the same graph, empty_dense layout, mode and
+    gather hint), each under `timeout -s KILL`:
+      1. `rocprofv3 --kernel-trace --stats`: the kernel's average duration on THIS box
+         (`kernel_trace_ms`, over `launches` dispatches after the plan-building one) -- the
+         profile that backs the line's own kernel time (VERDICT r04 item 2);
+      2. `--pmc FETCH_SIZE`, 3. `--pmc WRITE_SIZE` (separate passes, guide §PMC): HBM-side bytes
+         per launch, 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the gfx950 correction of
+         MI355X_MICROARCH.md:298), the mean over the launches after the plan-building one.
+    The bytes are L2->fabric bytes: reads the Infinity Cache serves are counted too (no gfx950
+    TCC counter separates them), so they bound the DRAM bytes from above.
+    keep_dir: copy the kernel-trace stats CSV there (`<tag>_kernel_stats.csv`)."""
     import shutil
     import subprocess
     import tempfile
@@ -232,35 +251,65 @@ def live_traffic(H, K: int, mode: str, timeout_s: int = 240) -> dict:
         return {"error": "rocprofv3 not found"}
     tmpd = tempfile.mkdtemp(prefix="gcg_pmc_")
     t0 = time.perf_counter()
+    out = {}
     try:
         graph = os.path.join(tmpd, "graph.npz")
         np.savez(graph, n=np.int64(H.shape[0]), indptr=H.indptr, indices=H.indices, data=H.data)
-        vals = {}
-        for c in PMC_COUNTERS:
-            cmd = ["timeout", "-s", "KILL", str(timeout_s), prof, "--pmc", c, "--output-format",
-                   "csv", "-d", os.path.join(tmpd, c), "-o", c, "--", sys.executable,
-                   os.path.join(ROOT, "tools", "pmc_probe.py"), graph, "--K", str(K),
-                   "--mode", mode]
+        probe = [sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), graph, "--K",
+                 str(K), "--mode", mode]
+
+        def run(name, prof_args, n_launch):
+            cmd = (["timeout", "-s", "KILL", str(timeout_s), prof] + prof_args +
+                   ["--output-format", "csv", "-d", os.path.join(tmpd, name), "-o", name, "--"] +
+                   probe + ["--launches", str(n_launch)])
             t1 = time.perf_counter()
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s + 30)
-            print(f"bench: live PMC {c} pass rc={r.returncode} in {time.perf_counter() - t1:.1f} s",
+            print(f"bench: live {name} pass rc={r.returncode} in {time.perf_counter() - t1:.1f} s",
                   file=sys.stderr, flush=True)
             if r.returncode != 0:
-                return {"error": f"{c} pass rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}"}
+                raise RuntimeError(f"{name} pass rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}")
+
+        # 1. kernel trace: the kernel's own duration on this box
+        try:
+            run("kt", ["--kernel-trace", "--stats"], launches)
+            ns = _read_kernel_trace(os.path.join(tmpd, "kt"))
+            if len(ns) < 2:
+                raise RuntimeError(f"kernel trace: {len(ns)} {PMC_KERNEL} dispatches")
+            ns = ns[1:]  # drop the plan-building call's launch
+            out["kernel_trace"] = {
+                "avg_ms": round(float(np.mean(ns)) / 1e6, 4),
+                "min_ms": round(min(ns) / 1e6, 4), "max_ms": round(max(ns) / 1e6, 4),
+                "dispatches": len(ns),
+                "source": "rocprofv3 --kernel-trace --stats of tools/pmc_probe.py (this run)"}
+            if keep_dir:
+                import glob
+                os.makedirs(keep_dir, exist_ok=True)
+                for fn in glob.glob(os.path.join(tmpd, "kt", "**", "*kernel_stats.csv"),
+                                    recursive=True):
+                    shutil.copy(fn, os.path.join(keep_dir, f"{tag}_kernel_stats.csv"))
+        except (OSError, subprocess.SubprocessError, RuntimeError, KeyError, ValueError) as exc:
+            out["kernel_trace"] = {"error": repr(exc)[:300]}
+        # 2, 3. the counters, one pass each
+        vals = {}
+        for c in PMC_COUNTERS:
+            run(c, ["--pmc", c], 4)
             v = _read_counter(os.path.join(tmpd, c), c)
             if len(v) < 2:
-                return {"error": f"{c}: {len(v)} {PMC_KERNEL} dispatches in the counter CSV"}
+                raise RuntimeError(f"{c}: {len(v)} {PMC_KERNEL} dispatches in the counter CSV")
             vals[c] = v[1:]  # drop the plan-building call's launch
         fetch = float(np.mean(vals["FETCH_SIZE"]))
         write = float(np.mean(vals["WRITE_SIZE"]))
-        return {"traffic": int(2 * fetch * 1024 + write * 1024),
-                "FETCH_SIZE_KiB_per_launch": round(fetch, 1),
-                "WRITE_SIZE_KiB_per_launch": round(write, 1),
-                "dispatches": {c: len(v) for c, v in vals.items()},
-                "spread": round(max(max(v) / min(v) for v in vals.values()) - 1, 4),
-                "gcg_source_hash": library_hash(), "pass_s": round(time.perf_counter() - t0, 1)}
-    except (OSError, subprocess.SubprocessError, KeyError, ValueError) as exc:
-        return {"error": repr(exc)[:300]}
+        out.update({"traffic": int(2 * fetch * 1024 + write * 1024),
+                    "FETCH_SIZE_KiB_per_launch": round(fetch, 1),
+                    "WRITE_SIZE_KiB_per_launch": round(write, 1),
+                    "dispatches": {c: len(v) for c, v in vals.items()},
+                    "spread": round(max(max(v) / min(v) for v in vals.values()) - 1, 4),
+                    "gcg_source_hash": library_hash(),
+                    "pass_s": round(time.perf_counter() - t0, 1)})
+        return out
+    except (OSError, subprocess.SubprocessError, RuntimeError, KeyError, ValueError) as exc:
+        out["error"] = repr(exc)[:300]
+        return out
     finally:
         shutil.rmtree(tmpd, ignore_errors=True)
 
@@ -339,6 +388,10 @@ def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev, H=None, live
            "roofline": roofline_record(B, k_ms, traffic, src, "spmm_rows_kernel")}
     if live and "error" in live:
         rec["live_pmc_error"] = live["error"]
+    kt = (live or {}).get("kernel_trace") or {}
+    if "avg_ms" in kt:
+        rec["roofline"]["kernel_trace_ms"] = kt["avg_ms"]
+        rec["roofline"]["kernel_trace"] = kt
     del A, Z, Y
     return rec
 
@@ -564,7 +617,8 @@ def exchange_ab(H, rank, world, dev, part, Zl, K, B, eff, timed, reps, args, m) 
     """One exchange of the A/B: the pipelined step with it, and the exchange alone."""
     from graphconvgeo_amd.distributed import RowPartitionedCSR
     alt = {}
-    pm = part if m == part.exchange else RowPartitionedCSR(H, rank, world, dev, exchange=m)
+    pm = part if m == part.exchange else RowPartitionedCSR(H, rank, world, dev, exchange=m,
+                                                           plan=part.plan)
     cm = pm._n_chunks(args.chunks, K)
     pm.chunk_buffers(K, cm).fill(Zl)
     Ym = gs.empty_dense(pm.n_local, K, dev)
@@ -605,6 +659,8 @@ def main():
     ap.add_argument("--no-live-pmc", dest="live_pmc", action="store_false",
                     help="N = 1: skip the live rocprofv3 PMC pass (traffic then comes from a "
                          "committed summary stamped with this library's source hash, if any)")
+    ap.add_argument("--profile-dir", default="",
+                    help="N = 1: keep the live kernel-trace stats CSVs there (e.g. gpurun_out/...)")
     ap.add_argument("--no-variants", dest="variants", action="store_false",
                     help="N = 1: skip the uniform-degree second run")
     ap.add_argument("--no-train-step", dest="train_step", action="store_false",
@@ -623,6 +679,9 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
+    ap.add_argument("--dist-timeout", type=float, default=600.0,
+                    help="N > 1: seconds a collective may take before the process group "
+                         "aborts and the run exits non-zero (distributed.init_process_group)")
     ap.add_argument("--no-alternatives", dest="alternatives", action="store_false",
                     help="N > 1: skip timing the feature-parallel alternative")
     ap.add_argument("--partitioned", action="store_true",
@@ -651,20 +710,23 @@ def main():
         if under_profiler():
             live = {"error": "skipped: this run is itself under rocprofv3"}
         else:
-            live = live_traffic(H, K, host_mode(H, args.mode))
+            live = live_traffic(H, K, host_mode(H, args.mode), keep_dir=args.profile_dir,
+                                tag="headline")
             if args.variants:
                 H_u = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind="uniform")
-                live_u = live_traffic(H_u, K, host_mode(H_u, args.mode))
+                live_u = live_traffic(H_u, K, host_mode(H_u, args.mode),
+                                      keep_dir=args.profile_dir, tag="uniform")
 
     dev_index = local_rank % max(torch.cuda.device_count(), 1)
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if world > 1:
         import torch.distributed as dist
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+
+        from graphconvgeo_amd.distributed import init_process_group
+        # explicit timeout + async error handling: a stuck collective ends the run non-zero
+        init_process_group(args.dist_backend, dev if args.dist_backend == "nccl" else None,
+                           timeout_s=args.dist_timeout)
         if dist.get_world_size() != world:
             raise SystemExit(f"process group has {dist.get_world_size()} ranks, WORLD_SIZE={world}")
 
@@ -753,7 +815,17 @@ def main():
         roofline = roofline_record(kbytes, k_ms, traffic, traffic_src,
                                    "spmm_rows_kernel (+ spmm_fixup_kernel)")
         if live:
+            kt = live.pop("kernel_trace", None) or {}
             roofline["live_pmc"] = live
+            if "avg_ms" in kt:
+                # the same launch under rocprofv3 --kernel-trace, same box, same run: backs the
+                # line's kernel time; a kernel cannot take longer than the step that runs it
+                roofline["kernel_trace_ms"] = kt["avg_ms"]
+                roofline["kernel_trace"] = kt
+                roofline["kernel_trace_vs_ms_per_step"] = round(kt["avg_ms"] / ms, 4)
+                roofline["kernel_trace_le_step"] = bool(kt["avg_ms"] <= ms * 1.02)
+            elif kt:
+                roofline["kernel_trace"] = kt
         # compulsory bytes (every array touched once) beside the edge-centric
         # count, so cache reuse on the gather is visible
         roofline["compulsory_bytes_per_launch"] = (

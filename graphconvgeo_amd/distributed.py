@@ -21,8 +21,9 @@ Three exchanges, chosen once at setup (`exchange=`), all into one operand layout
     H_p's remote columns map to n_local + searchsorted(halo, col). On a power-law
     Twitter-World graph the halo is 97 / 87 / 69 % of the remote rows at P = 2 / 4 / 8.
   "auto" picks halo when the largest halo fraction over all ranks is below 0.9, else allgather.
-All are pipelined over column chunks (count chosen per call, choose_chunks): every chunk's
-exchange is issued up front, chunk c's SpMM waits for its own. A producer may write its rows
+All are pipelined over column chunks (count chosen per call, choose_chunks, from every rank's
+numbers so that every rank issues the same collectives): every chunk's exchange is issued up
+front, chunk c's SpMM waits for its own. A producer may write its rows
 straight into the exchange buffers (chunk_buffers(...).own_views()), so the step copies nothing.
 Results are bitwise those of the unpartitioned SpMM (same per-row order).
 
@@ -96,6 +97,101 @@ def _wait(work):
         w.wait()
 
 
+DIST_TIMEOUT_S = 600.0
+
+
+def init_process_group(backend: str, device=None, timeout_s: float = DIST_TIMEOUT_S):
+    """torch.distributed.init_process_group for the row partition, made to fail rather than
+    hang: an explicit collective timeout, and (NCCL = RCCL) the async error handling that tears
+    the process down with a message when a collective exceeds it, so a stuck first RCCL run
+    ends non-zero instead of sitting until the driver's limit."""
+    import datetime
+    import os
+    if backend == "nccl":
+        # 1 = abort the communicator and tear the process down on a failed / timed-out
+        # collective (the watchdog thread raises; no rank is left waiting)
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        os.environ.setdefault("TORCH_NCCL_DUMP_ON_TIMEOUT", "0")
+    kw = {"timeout": datetime.timedelta(seconds=float(timeout_s))}
+    if backend == "nccl" and device is not None:
+        kw["device_id"] = torch.device(device)
+    dist.init_process_group(backend, **kw)
+    return dist.group.WORLD
+
+
+class PartitionPlan:
+    """The rank-independent structure of a 1-D row partition of the host H: the bounds, every
+    rank's halo (the remote rows its block references, sorted global ids), nonzeros and rows.
+    Every rank holds the whole host H, so every rank computes the same plan with no
+    communication; a single process building all P ranks (tests, tools) computes it once.
+    Decisions that must agree across ranks -- the exchange chosen by 'auto', the column-chunk
+    count (RowPartitionedCSR.choose_chunks) -- are taken from it, never from rank-local data."""
+
+    def __init__(self, H, world: int, bounds: Optional[np.ndarray] = None):
+        H = sps.csr_matrix(H)
+        if H.shape[0] != H.shape[1]:
+            raise ValueError("row partition expects a square graph operator")
+        self.H, self.world, self.n = H, int(world), H.shape[0]
+        self.bounds = row_partition(H.indptr, world) if bounds is None else np.asarray(bounds)
+        if self.bounds.size != world + 1:
+            raise ValueError("bounds must hold world + 1 entries")
+        b = self.bounds
+        self.rows = np.diff(b).astype(np.int64)
+        self.block_rows = int(self.rows.max()) if world > 0 else 0
+        ip = np.asarray(H.indptr, dtype=np.int64)
+        self.nnz = (ip[b[1:]] - ip[b[:-1]]).astype(np.int64)
+        self.halos = []
+        for q in range(world):
+            cols = np.unique(H.indices[ip[b[q]]:ip[b[q + 1]]])
+            self.halos.append(cols[(cols < b[q]) | (cols >= b[q + 1])].astype(np.int64))
+        remote_total = [max(self.n - int(self.rows[q]), 1) for q in range(world)]
+        self.halo_fraction = max((h.size / t for h, t in zip(self.halos, remote_total)),
+                                 default=0.0)
+
+    def resolve_exchange(self, exchange: str, halo_threshold: float = 0.9) -> str:
+        if exchange not in EXCHANGES:
+            raise ValueError(f"exchange must be one of {EXCHANGES}")
+        if exchange == "auto":
+            return "halo" if self.halo_fraction < halo_threshold else "allgather"
+        return exchange
+
+    def rows_in(self, exchange: str) -> np.ndarray:
+        """Rows every rank receives per exchange (index = rank)."""
+        P = self.world
+        if exchange == "allgather":
+            return np.full(P, (P - 1) * self.block_rows, dtype=np.int64)
+        if exchange == "mesh":
+            return int(self.rows.sum()) - self.rows
+        if exchange == "halo":
+            return np.array([h.size for h in self.halos], dtype=np.int64)
+        raise ValueError(f"exchange must be one of {EXCHANGES[1:]}")
+
+    def choose_chunks(self, exchange: str, K: int) -> int:
+        """Column chunks for one exchange + SpMM of width K, the same on every rank: 1 at world
+        1; otherwise the count minimising the SLOWEST rank's pipeline_time (every rank's
+        exchange bytes over min(P - 1, 7) xGMI links, every rank's local SpMM estimate), chunks
+        >= 64 columns. Every chunk is one collective per rank, so the count must agree: a
+        rank-local choice would issue different numbers and widths of collectives."""
+        if self.world == 1:
+            return 1
+        links = min(self.world - 1, 7)
+        w4 = (K + 3) // 4 * 4  # the exchange moves the padded width
+        t_x = self.rows_in(exchange) * w4 * 4 / (XGMI_LINK_GBPS * 1e9 * links)
+        t_s = [_spmm_bytes(int(r), int(z), K) / (LOCAL_SPMM_GBPS * 1e9)
+               for r, z in zip(self.rows, self.nnz)]
+        cmax = max(1, min(MAX_CHUNKS, K // MIN_CHUNK_COLS))
+
+        def worst(c):
+            return max(pipeline_time(float(x), s, c) for x, s in zip(t_x, t_s))
+        return min(range(1, cmax + 1), key=lambda c: (worst(c), c))
+
+
+def _as_ids(src) -> np.ndarray:
+    if isinstance(src, tuple):
+        return np.arange(src[0], src[1], dtype=np.int64)
+    return np.asarray(src, dtype=np.int64)
+
+
 def pipeline_time(t_exchange: float, t_spmm: float, chunks: int) -> float:
     """Modelled step time of `chunks` column chunks: exchanges back to back on the comm stream,
     chunk i's SpMM after its exchange and after chunk i-1's SpMM."""
@@ -121,8 +217,12 @@ class ExchangeLayout:
 
     def __init__(self, method: str, rank: int, world: int, group=None, counts=None,
                  pad: int = 0, n_own: int = 0, halo_rows: int = 0, send_index=None,
-                 send_counts=None, recv_counts=None):
+                 send_counts=None, recv_counts=None, sources=None):
         self.method, self.rank, self.world, self.group = method, rank, world, group
+        # sources: which global rows each slot holds (operand_ids) -- per rank q the global ids
+        # of its block's rows (allgather / mesh: an array or a (start, stop) range), or for
+        # halo (own global ids, halo global ids)
+        self.sources = sources
         if method in ("allgather", "mesh"):
             self.counts = [int(c) for c in counts]
             self.pad = int(pad)
@@ -138,6 +238,22 @@ class ExchangeLayout:
 
     def own(self, buf: torch.Tensor) -> torch.Tensor:
         return buf[self.own_off:self.own_off + self.n_own]
+
+    def operand_ids(self) -> np.ndarray:
+        """The global row each operand row holds after an exchange (-1: padding, never
+        referenced by the local operator) -- what the exchange must produce, so a single process
+        can build any rank's operand from the whole dense matrix (tests, tools)."""
+        if self.sources is None:
+            raise ValueError("this layout was built without its row sources")
+        ids = np.full(self.rows, -1, dtype=np.int64)
+        if self.method == "halo":
+            own, halo = self.sources
+            ids[:self.n_own] = _as_ids(own)
+            ids[self.n_own:] = _as_ids(halo)
+            return ids
+        for q, src in enumerate(self.sources):
+            ids[q * self.pad:q * self.pad + self.counts[q]] = _as_ids(src)
+        return ids
 
     def bytes_in(self, width: int) -> int:
         """Bytes this rank receives per exchange of `width` float columns."""
@@ -234,6 +350,13 @@ class _ChunkBuffers:
 # the exchanges and the local SpMMs of a step alone). None in normal runs.
 TRACE: Optional[list] = None
 
+# When set: a single-process rehearsal of one rank. pipelined_product calls
+# LOOPBACK(layout, buf, c0, c1) instead of the collective; the function writes what the exchange
+# would deliver into buf's remote rows (layout.operand_ids() names them). tests/
+# test_partition_world_gpu.py runs every rank of a P-way partition of the World graph in one
+# process this way. None in normal runs.
+LOOPBACK: Optional[Callable] = None
+
 
 def pipelined_product(spmm_into, A, bufs: _ChunkBuffers, out: torch.Tensor, bias=None,
                       gate=None, **kw) -> torch.Tensor:
@@ -243,7 +366,10 @@ def pipelined_product(spmm_into, A, bufs: _ChunkBuffers, out: torch.Tensor, bias
     output column is computed by the same kernel in the same storage order as unchunked."""
     if TRACE is not None:  # measurement hook (tools/bench_train_dist.py --phases)
         TRACE.append((spmm_into, A, bufs, out, bias, gate, dict(kw)))
-    works = [bufs.layout.exchange(buf, async_op=True) for _c0, _c1, buf in bufs.chunks]
+    if LOOPBACK is not None:
+        works = [LOOPBACK(bufs.layout, buf, c0, c1) for c0, c1, buf in bufs.chunks]
+    else:
+        works = [bufs.layout.exchange(buf, async_op=True) for _c0, _c1, buf in bufs.chunks]
     for (c0, c1, buf), work in zip(bufs.chunks, works):
         _wait(work)
         spmm_into(A, buf[:, :c1 - c0], out[:, c0:c1],
@@ -261,28 +387,27 @@ class RowPartitionedCSR:
 
     def __init__(self, H, rank: int, world: int, device, group=None,
                  local_spmm: Optional[Callable] = None, bounds: Optional[np.ndarray] = None,
-                 exchange: str = "auto", halo_threshold: float = 0.9):
-        H = sps.csr_matrix(H)
-        if H.shape[0] != H.shape[1]:
-            raise ValueError("row partition expects a square graph operator")
-        if exchange not in EXCHANGES:
-            raise ValueError(f"exchange must be one of {EXCHANGES}")
+                 exchange: str = "auto", halo_threshold: float = 0.9,
+                 plan: Optional[PartitionPlan] = None):
+        if plan is None:
+            plan = PartitionPlan(H, world, bounds)
+        elif plan.world != world or (bounds is not None and
+                                     not np.array_equal(np.asarray(bounds), plan.bounds)):
+            raise ValueError("plan was built for another partition")
+        H = plan.H
+        if not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
+        self.plan = plan
         self.rank, self.world, self.group = rank, world, group
         self.n = H.shape[0]
         self._indptr_host = H.indptr
-        self.bounds = row_partition(H.indptr, world) if bounds is None else np.asarray(bounds)
+        self.bounds = plan.bounds
         self.start, self.stop = int(self.bounds[rank]), int(self.bounds[rank + 1])
-        self.block_rows = int(np.diff(self.bounds).max()) if world > 0 else 0
+        self.block_rows = plan.block_rows
         b = self.bounds
-        # halo (remote rows referenced) of every rank's block, sorted global ids
-        halos = []
-        for q in range(world):
-            cols = np.unique(H.indices[H.indptr[b[q]]:H.indptr[b[q + 1]]])
-            halos.append(cols[(cols < b[q]) | (cols >= b[q + 1])])
-        remote_total = [max(self.n - (b[q + 1] - b[q]), 1) for q in range(world)]
-        self.halo_fraction = max((h.size / t for h, t in zip(halos, remote_total)), default=0.0)
-        if exchange == "auto":
-            exchange = "halo" if self.halo_fraction < halo_threshold else "allgather"
+        halos = plan.halos
+        self.halo_fraction = plan.halo_fraction
+        exchange = plan.resolve_exchange(exchange, halo_threshold)
         self.exchange = exchange
         local = H[self.start:self.stop]
         self.local_global = local  # global column ids (target-row backward operators)
@@ -291,7 +416,8 @@ class RowPartitionedCSR:
             cols = remap_columns(local.indices, self.bounds, self.block_rows)
             ncols = world * self.block_rows
             self.layout = ExchangeLayout(exchange, rank, world, group, counts=np.diff(self.bounds),
-                                         pad=self.block_rows)
+                                         pad=self.block_rows,
+                                         sources=[(int(b[q]), int(b[q + 1])) for q in range(world)])
         else:
             halo = halos[rank]
             own = (local.indices >= self.start) & (local.indices < self.stop)
@@ -312,7 +438,8 @@ class RowPartitionedCSR:
             self.layout = ExchangeLayout("halo", rank, world, group, n_own=self.n_local,
                                          halo_rows=self.halo_rows, send_index=self.send_index,
                                          send_counts=self.send_counts,
-                                         recv_counts=self.recv_counts)
+                                         recv_counts=self.recv_counts,
+                                         sources=((self.start, self.stop), halo))
         local = sps.csr_matrix((local.data, cols, local.indptr),
                                shape=(self.stop - self.start, ncols))
         self.local_host = local
@@ -327,7 +454,6 @@ class RowPartitionedCSR:
             self._spmm = local_spmm
             self._on_device = False
         self._bufs = {}
-        self._target_ops = {}
         self.chunks_override = None
 
     def resolve_mode(self, mode: str = "auto") -> str:
@@ -377,16 +503,10 @@ class RowPartitionedCSR:
 
     # -- chunk count ----------------------------------------------------------------------
     def choose_chunks(self, K: int) -> int:
-        """Column chunks for one exchange + SpMM of width K: 1 when there is nothing to hide
-        (world 1); otherwise the count minimising pipeline_time for this rank's exchange bytes
-        (over min(P - 1, 7) xGMI links) against its local SpMM estimate, chunks >= 64 columns."""
-        if self.world == 1:
-            return 1
-        links = min(self.world - 1, 7)
-        t_x = self.exchange_bytes_per_row(K) / (XGMI_LINK_GBPS * 1e9 * links)
-        t_s = _spmm_bytes(self.n_local, self.nnz_local, K) / (LOCAL_SPMM_GBPS * 1e9)
-        cmax = max(1, min(MAX_CHUNKS, K // MIN_CHUNK_COLS))
-        return min(range(1, cmax + 1), key=lambda c: (pipeline_time(t_x, t_s, c), c))
+        """Column chunks for one exchange + SpMM of width K (PartitionPlan.choose_chunks): the
+        same count on every rank -- decided from every rank's exchange bytes and local SpMM,
+        which every rank derives from the host H -- so all ranks issue the same collectives."""
+        return self.plan.choose_chunks(self.exchange, K)
 
     def _n_chunks(self, n_chunks, K: int) -> int:
         if n_chunks in (None, "auto", 0):  # chunks_override: a fixed count for 'auto' callers
@@ -452,10 +572,13 @@ class RowPartitionedCSR:
 
     # -- the gradient of a target-row subset ---------------------------------------------------
     def target_backward(self, targets: "TargetRows") -> "TargetRowsBackward":
-        op = self._target_ops.get(id(targets))
-        if op is None or op.targets is not targets:
+        """The target list's backward operator, cached ON the list (a cache on the
+        partition keyed by id() kept every list that ever reached backward -- and its device
+        operator and chunk buffers -- alive; now they go with the list)."""
+        op = getattr(targets, "_backward_op", None)
+        if op is None or op.part is not self:
             op = TargetRowsBackward(self, targets)
-            self._target_ops[id(targets)] = op
+            targets._backward_op = op
         return op
 
 
@@ -532,7 +655,7 @@ class TargetRowsBackward:
         mean = sum(counts) / max(len(counts), 1)
         method = "mesh" if part.exchange == "mesh" or max(counts) > 1.25 * mean else "allgather"
         self.layout = ExchangeLayout(method, part.rank, part.world, part.group, counts=counts,
-                                     pad=pad)
+                                     pad=pad, sources=targets.block_distinct)
         if part._on_device:
             from .sparse import DeviceCSR
             self.A = DeviceCSR.from_scipy(A, part.device)

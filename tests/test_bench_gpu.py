@@ -45,6 +45,9 @@ def test_bench_single_gpu_line(cuda):
     assert "traffic" in rf["live_pmc"], rf["live_pmc"]
     assert rf["traffic"] == rf["live_pmc"]["traffic"] > 0 and 0 < rf["frac"] <= 1
     assert rf["edge_centric_achieved"] > 0 and rf["frac_vs_achievable"] > 0
+    # the same launch under rocprofv3 --kernel-trace in the same run backs the kernel time
+    assert rf["kernel_trace_ms"] > 0 and rf["kernel_trace"]["dispatches"] >= 1, rf.get("kernel_trace")
+    assert "kernel_trace_le_step" in rf
     assert rec["variants"]["uniform"]["roofline"]["traffic"] > 0
     assert rec["variants"]["uniform"]["kernel_ms"] > 0 and rec["variants"]["k1500"]["kernel_ms"] > 0
     # the like-for-like point of the scaling series: the same SpMM in the mode N > 1 runs

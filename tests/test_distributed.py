@@ -23,6 +23,30 @@ def _free_port():
     return p
 
 
+def _run_world(target, world, *args, results: int = 1, timeout: float = 180):
+    """Spawn `world` gloo ranks of target(rank, world, port, *args, q); returns the `results`
+    items the ranks put on q. Ranks still alive afterwards (a mismatched collective hangs) are
+    killed, so a failing case cannot leave processes behind."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, world, port) + tuple(args) + (q,))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        out = [q.get(timeout=timeout) for _ in range(results)]
+        for p in procs:
+            p.join(timeout=60)
+            assert p.exitcode == 0
+    finally:
+        for p in procs:
+            if p.is_alive():
+                p.kill()
+                p.join(timeout=10)
+    return out
+
+
 def _oracle_spmm(A, Z_full, out=None, bias=None, act=None, rows=None, gate=None, **kw):
     """Test-only rank-local SpMM: the CPU oracle with the HIP entry's epilogue arguments."""
     from oracle import gcn_oracle as O
@@ -38,7 +62,7 @@ def _oracle_spmm(A, Z_full, out=None, bias=None, act=None, rows=None, gate=None,
     return Y
 
 
-def _worker(rank, world, port, n, e, K, q, exchange):
+def _worker(rank, world, port, n, e, K, exchange, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -68,6 +92,12 @@ def _worker(rank, world, port, n, e, K, q, exchange):
         gate1 = torch.empty_like(gate)
         part.spmm_pipelined(Zl, Yr1, n_chunks=1, bias=bias, act="relu", gate=gate1)
         assert torch.equal(Yr, Yr1) and torch.equal(gate, gate1)
+        # the exchange delivers exactly the rows layout.operand_ids() names (the single-process
+        # rehearsal, distributed.LOOPBACK, builds operands from it)
+        ids = part.layout.operand_ids()
+        full = part.all_gather(Zl).numpy()
+        ok = ids >= 0
+        assert np.array_equal(full[ok], Z[ids[ok]]) and ids.size == part.operand_rows()
         out = [None] * world
         dist.all_gather_object(out, (part.start, part.stop, Y.numpy()))
         if rank == 0:
@@ -77,20 +107,11 @@ def _worker(rank, world, port, n, e, K, q, exchange):
 
 
 @pytest.mark.parametrize("exchange", ["allgather", "mesh", "halo"])
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_row_partitioned_spmm_equals_full(world, exchange):
     from oracle import gcn_oracle as O
     n, e, K = 3000, 20000, 24
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, n, e, K, q, exchange)) for r in range(world)]
-    for p in procs:
-        p.start()
-    out = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    (out,) = _run_world(_worker, world, n, e, K, exchange)
     H = synthetic_graph(n, e)
     Z = np.random.default_rng(5).standard_normal((n, K)).astype(np.float32)
     ref = O.spmm_f32(H, Z)
@@ -169,7 +190,7 @@ class _CPUOps:
         return torch.from_numpy(out)
 
 
-def _prop_worker(rank, world, port, n, e, K, q, exchange):
+def _prop_worker(rank, world, port, n, e, K, exchange, hi, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
@@ -179,7 +200,7 @@ def _prop_worker(rank, world, port, n, e, K, q, exchange):
         rng = np.random.default_rng(11)
         Z = rng.standard_normal((n, K)).astype(np.float32)
         b = rng.standard_normal(K).astype(np.float32)
-        targets = rng.integers(0, n, size=n // 2).astype(np.int32)  # duplicates included
+        targets = rng.integers(0, hi, size=n // 2).astype(np.int32)  # duplicates included
         part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm, exchange=exchange)
         part.chunks_override = 3 if world == 3 else None  # the pipelined form in fwd and bwd
         Zp = torch.from_numpy(part.local_rows(Z).copy()).requires_grad_()
@@ -194,9 +215,10 @@ def _prop_worker(rank, world, port, n, e, K, q, exchange):
         # only the distinct targets' rows travel; the operator keeps only their columns
         assert bwd.layout.counts == [d.size for d in tg.block_distinct]
         assert bwd.nnz <= part.nnz_local
+        assert tg._backward_op is bwd  # cached on the list, not on the partition
         out = [None] * world
         dist.all_gather_object(out, (part.start, part.stop, pos, P.detach().numpy(),
-                                     Zp.grad.numpy(), bt.grad.numpy()))
+                                     Zp.grad.numpy(), bt.grad.numpy(), len(tg)))
         if rank == 0:
             q.put(out)
     finally:
@@ -204,29 +226,25 @@ def _prop_worker(rank, world, port, n, e, K, q, exchange):
 
 
 @pytest.mark.parametrize("exchange,world", [("allgather", 2), ("halo", 2), ("mesh", 2),
-                                            ("mesh", 3), ("allgather", 3)])
+                                            ("mesh", 3), ("allgather", 3), ("allgather", 4),
+                                            ("halo", 4), ("mesh", 4), ("allgather", 8),
+                                            ("halo", 8), ("mesh", 8)])
 def test_partitioned_propagate_fwd_bwd(exchange, world):
     """Two stacked partitioned propagates (rectify, then a target-row subset with duplicates)
     and their backward through H's symmetry: activations and input gradients bitwise equal to
-    the single-process oracle chain; the bias gradient (a cross-rank sum) within fp32."""
+    the single-process oracle chain; the bias gradient (a cross-rank sum) within fp32. At world
+    4 and 8 the targets lie in the first 40 % of the nodes (the reference's train rows come
+    first): the last ranks hold no target, contribute no rows to the target exchange, and still
+    receive the others'."""
     from oracle import gcn_oracle as O
     n, e, K = 2500, 16000, 12
-    ctx = mp.get_context("spawn")
-    q = ctx.Queue()
-    port = _free_port()
-    procs = [ctx.Process(target=_prop_worker, args=(r, world, port, n, e, K, q, exchange))
-             for r in range(world)]
-    for p in procs:
-        p.start()
-    out = q.get(timeout=120)
-    for p in procs:
-        p.join(timeout=60)
-        assert p.exitcode == 0
+    hi = n if world < 4 else int(0.4 * n)
+    (out,) = _run_world(_prop_worker, world, n, e, K, exchange, hi)
     H = synthetic_graph(n, e)
     rng = np.random.default_rng(11)
     Z = rng.standard_normal((n, K)).astype(np.float32)
     b = rng.standard_normal(K).astype(np.float32)
-    targets = rng.integers(0, n, size=n // 2).astype(np.int32)
+    targets = rng.integers(0, hi, size=n // 2).astype(np.int32)
     R = rng.standard_normal((targets.size, K)).astype(np.float32)
     h = O.spmm_f32(H, Z, bias=b, act="relu")
     P = O.spmm_f32(H, h, rows=targets)
@@ -238,13 +256,74 @@ def test_partitioned_propagate_fwd_bwd(exchange, world):
     got_P = np.zeros_like(P)
     got_gZ = np.zeros_like(g_Z)
     g_b = np.zeros(K, np.float64)
-    for start, stop, pos, Pp, gZp, gbp in out:
+    n_targets = []
+    for start, stop, pos, Pp, gZp, gbp, nt in out:
         got_P[pos] = Pp
         got_gZ[start:stop] = gZp
         g_b += gbp
+        n_targets.append(nt)
     assert np.array_equal(got_P, P)
     assert np.array_equal(got_gZ, g_Z)
     assert np.allclose(g_b, g_pre.astype(np.float64).sum(0), rtol=1e-5, atol=1e-4)
+    assert sum(n_targets) == targets.size
+    if world >= 4:
+        assert n_targets[-1] == 0  # a rank with no targets
+
+
+def _chunk_agree_worker(rank, world, port, K, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from graphconvgeo_amd.distributed import RowPartitionedCSR
+        H, bounds = _unequal_graph()
+        Z = np.random.default_rng(7).standard_normal((H.shape[0], K)).astype(np.float32)
+        part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm,
+                                 exchange="halo", bounds=bounds)
+        c = part.choose_chunks(K)
+        Zl = torch.from_numpy(part.local_rows(Z).copy())
+        Y = torch.empty((part.n_local, K))
+        part.spmm_pipelined(Zl, Y, n_chunks="auto")  # one all_to_all per chunk on every rank
+        out = [None] * world
+        dist.all_gather_object(out, (rank, c, part.halo_rows, part.start, part.stop, Y.numpy()))
+        if rank == 0:
+            q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
+def _unequal_graph():
+    """A 2000-node power-law graph plus 1000 isolated self-loop nodes, split into unequal
+    blocks: the last rank's block references no remote row (its halo is empty)."""
+    import scipy.sparse as sps
+    H = sps.block_diag((synthetic_graph(2000, 12000), sps.identity(1000, dtype=np.float32)),
+                       format="csr").astype(np.float32)
+    return H, np.array([0, 500, 1400, 2000, 3000])
+
+
+def test_auto_chunks_agree_across_ranks():
+    """the auto column-chunk count must be the same on every rank, or ranks
+    issue different numbers and widths of collectives. Unequal blocks, halo exchange, K = 136
+    (2 chunks possible), and one rank with an empty halo -- whose own numbers alone would say
+    'nothing to hide, 1 chunk' while the others want 2. Every rank picks the same count and
+    the pipelined product equals the unpartitioned one."""
+    from oracle import gcn_oracle as O
+    from graphconvgeo_amd.distributed import PartitionPlan, pipeline_time
+    K, world = 136, 4
+    H, bounds = _unequal_graph()
+    plan = PartitionPlan(H, world, bounds)
+    assert plan.rows_in("halo")[-1] == 0
+    # the rank-local model of round 4 would disagree here (the premise of the test)
+    assert pipeline_time(0.0, 1.0, 1) < pipeline_time(0.0, 1.0, 2)
+    (out,) = _run_world(_chunk_agree_worker, world, K)
+    chunks = {c for _r, c, *_ in out}
+    assert len(chunks) == 1 and chunks == {plan.choose_chunks("halo", K)} == {2}
+    assert out[-1][2] == 0  # the last rank's halo is empty
+    Z = np.random.default_rng(7).standard_normal((H.shape[0], K)).astype(np.float32)
+    ref = O.spmm_f32(H, Z)
+    got = np.zeros_like(ref)
+    for _r, _c, _h, start, stop, Y in out:
+        got[start:stop] = Y
+    assert np.array_equal(got, ref)
 
 
 def test_local_targets_keeps_order_and_duplicates():

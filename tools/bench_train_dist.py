@@ -51,10 +51,8 @@ def main():
     torch.cuda.set_device(dev_index)
     dev = torch.device("cuda", dev_index)
     if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=dev)
-        else:
-            dist.init_process_group("gloo")
+        from graphconvgeo_amd.distributed import init_process_group
+        init_process_group(args.dist_backend, dev if args.dist_backend == "nccl" else None)
     cfg = CONFIGS[args.config]
     t0 = time.perf_counter()
     H = synthetic_graph(cfg.n_nodes, cfg.n_edges)
