@@ -425,16 +425,10 @@ def dense_kernels_bench(reps: int, dev) -> dict:
         "gemm_nt f32 MFMA: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP, math="f32"),
         "gemm_tn: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G),
         "fused: P.W2 + b2 -> softmax-CE, hits, dlogits (mlpconv.py:88-95)":
-            lambda: fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits, math="bf16x6"),
+            lambda: dense._fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits, math="bf16x6"),
         "fused f32 MFMA: P.W2 + b2 -> softmax-CE, hits, dlogits":
-            lambda: fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits, math="f32"),
+            lambda: dense._fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits, math="f32"),
     }
-    def fused(*a, math):
-        os.environ["GCG_FUSED_MATH"] = math  # read per launch by gcg_project_softmax_xent_*
-        try:
-            dense._fused(*a)
-        finally:
-            os.environ.pop("GCG_FUSED_MATH", None)
 
     flops = 2.0 * T * K * C
     out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,

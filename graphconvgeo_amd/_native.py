@@ -90,10 +90,26 @@ SIGNATURES = {
     "gcg_softmax_xent_weighted_f32": (C.c_int, [_i64, _i64, _p, _i64, _p, C.c_float, _p, _p, _i64,
                                                 _p, _p, _p, _p]),
     "gcg_gemm_tn_f32_workspace_bytes": (C.c_int, [_i64, _i64, _i64, _psz]),
+    # round 5: the arithmetic (GCG_MATH_*) and the tile are per-call arguments
+    "gcg_dense_tile_count": (C.c_int32, [C.c_int32, C.c_int32]),
+    "gcg_gemm": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, C.c_int, _p, _i64, C.c_int32,
+                           C.c_int32, _p]),
+    "gcg_gemm_nt": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, C.c_int, _p, _i64,
+                              C.c_int32, C.c_int32, _p, _i64, _p]),
+    "gcg_gemm_nt_workspace": (_i64, [_i64, _i64, C.c_int32]),
+    "gcg_project_softmax_xent": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p,
+                                           C.c_float, _p, _p, _i64, _p, _p, _p, C.c_int32,
+                                           C.c_int32, _p, _i64, _p]),
+    "gcg_project_softmax_xent_workspace": (_i64, [_i64, _i64, C.c_int32]),
+    "gcg_gemm_tn_workspace_bytes": (C.c_int, [_i64, _i64, _i64, C.c_int32, C.c_int32, _psz]),
+    "gcg_gemm_tn": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, C.c_int32,
+                              C.c_int32, _p, C.c_size_t, _p]),
     "gcg_gemm_tn_f32": (C.c_int, [_i64, _i64, _i64, _p, _i64, _p, _i64, _p, _p, _i64, _p,
                                   C.c_size_t, _p]),
     "gcg_spgemm": (C.c_int, [_i64, _i64, _i64, _i64, _p, _p, _p, C.c_int, _i64, _p, _p, _p,
                              C.c_int, _i64, _p, _p, _p, _p, _p]),
+    "gcg_spgemm_ex": (C.c_int, [_i64, _i64, _i64, _i64, _p, _p, _p, C.c_int, _i64, _p, _p, _p,
+                                C.c_int, _i64, _p, _p, _p, _p, C.c_int32, _i64, _p]),
 }
 
 _lock = threading.Lock()

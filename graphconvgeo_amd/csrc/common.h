@@ -36,10 +36,6 @@ inline int bits_for(int64_t n) {
   while (b < 31 && (int64_t{1} << b) < n) ++b;
   return b;
 }
-inline int env_int(const char* name) {
-  const char* e = std::getenv(name);
-  return e ? std::atoi(e) : 0;
-}
 
 namespace {  // small device helpers, one copy per translation unit
 

@@ -51,7 +51,8 @@ __device__ __forceinline__ f4 mfma4(float a, float b, f4 c) {
 // |x1| <= 2^-9 |x|, |x2| <= 2^-17 |x|, x - (x0 + x1 + x2) <= 2^-26 |x|). a . b keeps the six
 // plane products of order <= 2^-16 -- a0b0, a0b1, a1b0, a0b2, a1b1, a2b0 -- each exact in the
 // f32 accumulator; the dropped a1b2 + a2b1 + a2b2 are <= 2^-25 |a||b|, below f32 rounding. NaN
-// propagates (through plane 0 and the NaN residuals); an infinite operand gives NaN, not +-Inf.
+// propagates (through plane 0 and the NaN residuals); an infinite or > 3.39e38 operand gives a
+// non-finite tile, which f32_tile below recomputes with f32 products (f32 semantics).
 using f8 = __attribute__((ext_vector_type(8))) float;
 using bf8 = __attribute__((ext_vector_type(8))) __bf16;
 
@@ -82,6 +83,66 @@ __device__ __forceinline__ void split3(const f8 x, bf8& h0, bf8& h1, bf8& h2) {
 }
 __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// f32 semantics for the bf16x6 kernels (round 5). Three bf16 planes cannot carry an infinite
+// operand (plane 0 = +-Inf, the residual Inf - Inf = NaN) nor one above bf16's largest finite
+// value, 3.39e38 < FLT_MAX (plane 0 rounds to Inf); either leaves a NaN or Inf in the wave's
+// accumulators, and so does a product or sum that overflows. A wave whose tile holds any
+// non-finite value after the K loop (a wave-uniform ballot) recomputes its tile with f32 MFMA
+// products (v_mfma_f32_16x16x4_f32) straight from global memory, in the f32 kernels' k order
+// (16-deep steps, step s takes k = k0 + 4q + s, k >= K zeroed): Inf propagates, Inf * 0 and
+// Inf - Inf give NaN, overflow gives Inf -- the f32 MFMA kernel's result for that tile. Finite
+// data of sane range never takes the branch (~1 v_cmp_class per accumulator element).
+template <int RT, int G>
+__device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4]) {
+  bool bad = false;
+#pragma unroll
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(acc[t][g][e][r]);
+  return __builtin_amdgcn_ballot_w64(bad) != 0;
+}
+// B element (k, column n) at B + n * bn + k * bk (NT: Bt, bn = ldbt, bk = 1; fused: W, bn = 1,
+// bk = ldw). rowb = the first row of the wave's 16 RT-row band; columns colw + 64 g + 4 j + e.
+template <int RT, int G>
+__device__ __forceinline__ void f32_tile(f4 (&acc)[RT][G][4], int M, int N, int K,
+                                         const float* __restrict__ A, int64_t lda, int64_t rowb,
+                                         const float* __restrict__ B, int64_t bn, int64_t bk,
+                                         int colw, int j, int q) {
+  int64_t ar[RT];
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    const int64_t r = rowb + 16 * t + j;
+    ar[t] = (r < M ? r : M - 1) * lda;
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc[t][g][e] = f4{0.f, 0.f, 0.f, 0.f};
+  }
+  for (int k0 = 0; k0 < K; k0 += 16) {
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const int k = k0 + 4 * q + s;
+      const bool kin = k < K;
+      float a[RT];
+#pragma unroll
+      for (int t = 0; t < RT; ++t) a[t] = kin ? A[ar[t] + k] : 0.f;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = colw + 64 * g + 4 * j + e;
+          const float b = (kin && c < N) ? B[c * bn + static_cast<int64_t>(k) * bk] : 0.f;
+#pragma unroll
+          for (int t = 0; t < RT; ++t) acc[t][g][e] = mfma4(a[t], b, acc[t][g][e]);
+        }
+    }
+  }
 }
 
 template <int W>
@@ -864,6 +925,10 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       }
     }
   }
+  if constexpr (MX != 0) {  // bf16x6: f32 semantics for Inf / huge operands (f32_tile)
+    if (tile_nonfinite<RT, G>(acc))
+      f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldb, 1, colw, j, q);
+  }
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
@@ -942,7 +1007,7 @@ struct Nt3Cfg {
 template <int RT, int G, int WR, int WC, int S>
 __global__ __launch_bounds__(64 * WR * WC, (Nt3Cfg<RT, G, WR, WC, S>::OCC)) void
 gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
-                const unsigned* __restrict__ Bs, const float* __restrict__ bias, int act,
+                const unsigned* __restrict__ Bs, const float* __restrict__ Bt, int64_t ldbt, const float* __restrict__ bias, int act,
                 float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
   using Cfg = Nt3Cfg<RT, G, WR, WC, S>;
   constexpr int EPI = 0;
@@ -1100,6 +1165,8 @@ gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
         }
       }
   }
+  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+    f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
@@ -1130,7 +1197,7 @@ struct Nt3rCfg {
 template <int RT, int G, int WR, int WC>
 __global__ __launch_bounds__(64 * WR * WC, (Nt3rCfg<RT, G, WR, WC>::OCC)) void
 gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
-                 const unsigned* __restrict__ Bs, const float* __restrict__ bias, int act,
+                 const unsigned* __restrict__ Bs, const float* __restrict__ Bt, int64_t ldbt, const float* __restrict__ bias, int act,
                  float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
   using Cfg = Nt3rCfg<RT, G, WR, WC>;
   constexpr int EPI = 0;
@@ -1281,6 +1348,8 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     step(c, alo, ahi, blo, bhi);
     if (c + 1 < Kc) step(c + 1, blo, bhi, alo, ahi);
   }
+  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+    f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
@@ -1553,6 +1622,8 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       if (c + 1 < Kc) chunk(c + 1, w1, w0);
     }
   }
+  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+    f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, B, 1, ldb, colw, j, q);
 #define GCG_EPI_BV_READY
 #define GCG_EPI_LABELS_LDS
   f4 bv[G];
@@ -1845,7 +1916,20 @@ struct TnPlan {
   int mt, nt, S, rows_per_split, Mp, Np;
 };
 
-TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
+// Alternative split-K layouts (gcg_gemm_tn tile 1..n): {MG, NG, PD, WM, OCC}. tools/exp_tn_*.py
+// measured each; the default below is a function of the shape only.
+constexpr int kTnTiles[][5] = {
+    {1, 2, 8, 1, 0},   // 1: round-2 workgroup tiles (4 waves side by side, 64 x 256 NG)
+    {1, 3, 8, 0, 0},   // 2: per-wave 64 x 192, 1 wave per SIMD, 8-deep ring
+    {1, 2, 8, 0, 0},   // 3: per-wave 64 x 128, 1 wave per SIMD
+    {1, 3, 12, 0, 0},  // 4: per-wave 64 x 192, 12-deep ring
+    {1, 1, 8, 4, 0},   // 5: 4 waves stacked along M
+    {1, 3, 3, 0, 2},   // 6: per-wave 64 x 192, 2 waves per SIMD (the default at N = 930)
+    {1, 2, 6, 0, 2},   // 7: per-wave 64 x 128, 2 waves per SIMD
+};
+constexpr int kTnTileCount = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
+
+TnPlan tn_plan(int64_t R, int64_t M, int64_t N, int tile = 0) {
   TnPlan p;
   // Default: per-wave 64 x 64*NG tiles (WM = 0), NG = 3 or 2, whichever pads N less (ties: 3,
   // fewer loads per MFMA). The round-2 workgroup tiles (WM = 1: 4 waves side by side, 64 x
@@ -1870,15 +1954,9 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // 300 x 930 dW2 (73-82 vs 106 TFLOP/s: its 8-15 N tiles re-read A), tools/exp_tn_layout.py.
   const bool stacked = M <= 256 && M % 64 == 0 && N <= 512;
   if (stacked) p.ng = 1, p.pd = 8, p.occ = 0, p.wm = static_cast<int>(M / 64), slots = 2048;
-  // experiment knobs: "MG,NG,PD[,WM[,OCC]]" (GCG_TN_NOT_STACKED=1: leave the stacked shapes
-  // alone; GCG_TN_STACKED: a layout for the stacked shapes only)
-  const char* v = std::getenv("GCG_TN");
-  if (v && stacked && env_int("GCG_TN_NOT_STACKED")) v = nullptr;
-  if (const char* vs = std::getenv("GCG_TN_STACKED"); vs && stacked) v = vs;
-  if (v) {
-    int a = 0, b = 0, c = 0, d = 1, e = 0;
-    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) >= 3)
-      p.mg = a, p.ng = b, p.pd = c, p.wm = d, p.occ = e, slots = 2048;
+  if (tile > 0) {  // an explicit alternative (caller-checked range)
+    const int* t = kTnTiles[tile - 1];
+    p.mg = t[0], p.ng = t[1], p.pd = t[2], p.wm = t[3], p.occ = t[4], slots = 2048;
   }
   const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
   const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
@@ -1887,7 +1965,6 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N) {
   // ~`slots` tiles per launch (2048: 2 workgroups per CU of the 256 CUs; per-wave tiles at 1
   // wave per SIMD: 2 rounds of the 1024 SIMDs -- 1 round measured the same speed with 2x longer
   // serial sums), at least 256 rows per split, 16-row aligned
-  if (const char* v = std::getenv("GCG_TN_SLOTS")) slots = std::max(1, std::atoi(v));  // knob
   const int64_t want = std::max<int64_t>(1, slots / std::max(1, p.mt * p.nt));
   const int64_t max_s = std::max<int64_t>(1, R / 256);
   p.S = static_cast<int>(std::min(want, max_s));
@@ -1911,8 +1988,11 @@ struct Shape {
   int bn() const { return 64 * G * WC; }
 };
 
-// Instantiated tiles. Row-band (WC = 4) tiles keep a whole output row of up to 1024
-// columns in one workgroup (needed by the fused softmax); WR = 4 tiles serve narrow N.
+// Instantiated tiles. EPI = 0 (plain products): the LDS-B tiles (gemm_bl_kernel, the default)
+// and the register-B tiles (gcg_gemm tile 1). EPI = 1 (the fused output layer on the f32 MFMA):
+// row bands keeping a whole output row of up to 1024 columns in one workgroup, the B register
+// set split into PF rotating parts (the default 8 at G = 4, 4 below; gcg_project_softmax_xent
+// tiles 1..5 = 0, 2, 4, 8, 16 parts).
 template <int EPI>
 gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, int K,
                        const float* A, int64_t lda, const float* B, int64_t ldb,
@@ -1927,14 +2007,6 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
-  GCG_GEMM_BL_CASE(4, 4)
-  GCG_GEMM_BL_CASE(4, 2)
-  GCG_GEMM_BL_CASE(5, 1)
-  GCG_GEMM_BL_CASE(4, 1)
-  GCG_GEMM_BL_CASE(3, 1)
-  GCG_GEMM_BL_CASE(2, 1)
-  GCG_GEMM_BL_CASE(1, 1)
-#undef GCG_GEMM_BL_CASE
 #define GCG_GEMM_CASE(rt, g, wr, wc, pf)                                                    \
   if (!s.BL && s.RT == rt && s.G == g && s.WR == wr && s.WC == wc && s.PF == pf) {           \
     hipLaunchKernelGGL((gemm_kernel<rt, g, wr, wc, EPI, pf>), grid, dim3(64 * (wr) * (wc)), 0, \
@@ -1944,79 +2016,74 @@ gcg_status launch_gemm(const Shape& s, dim3 grid, hipStream_t st, int M, int N, 
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
-  GCG_GEMM_CASE(2, 1, 1, 4, 1)
-  GCG_GEMM_CASE(2, 2, 1, 4, 1)
-  GCG_GEMM_CASE(2, 3, 1, 4, 1)
-  GCG_GEMM_CASE(2, 4, 1, 4, 1)
-  GCG_GEMM_CASE(4, 4, 1, 4, 1)
-  GCG_GEMM_CASE(4, 2, 1, 4, 1)
-  GCG_GEMM_CASE(4, 3, 1, 4, 1)
-  GCG_GEMM_CASE(2, 4, 1, 4, 0)
-  GCG_GEMM_CASE(2, 2, 1, 4, 0)
-  GCG_GEMM_CASE(2, 3, 1, 4, 0)
-  GCG_GEMM_CASE(2, 4, 2, 4, 0)
-  GCG_GEMM_CASE(2, 4, 1, 4, 2)
-  GCG_GEMM_CASE(2, 3, 1, 4, 2)
-  GCG_GEMM_CASE(2, 2, 1, 4, 2)
-  GCG_GEMM_CASE(2, 4, 1, 4, 4)
-  GCG_GEMM_CASE(2, 4, 1, 4, 8)
-  GCG_GEMM_CASE(2, 4, 1, 4, 16)
-  GCG_GEMM_CASE(2, 3, 1, 4, 4)
-  GCG_GEMM_CASE(2, 2, 1, 4, 4)
-  GCG_GEMM_CASE(2, 1, 4, 1, 1)
-  GCG_GEMM_CASE(2, 2, 4, 1, 1)
-  GCG_GEMM_CASE(2, 3, 4, 1, 1)
-  GCG_GEMM_CASE(2, 4, 4, 1, 1)
-  GCG_GEMM_CASE(2, 5, 4, 1, 1)
+  if constexpr (EPI == 0) {
+    GCG_GEMM_BL_CASE(4, 4)
+    GCG_GEMM_BL_CASE(4, 2)
+    GCG_GEMM_BL_CASE(5, 1)
+    GCG_GEMM_BL_CASE(4, 1)
+    GCG_GEMM_BL_CASE(3, 1)
+    GCG_GEMM_BL_CASE(2, 1)
+    GCG_GEMM_BL_CASE(1, 1)
+    GCG_GEMM_CASE(4, 4, 1, 4, 1)
+    GCG_GEMM_CASE(4, 2, 1, 4, 1)
+    GCG_GEMM_CASE(4, 3, 1, 4, 1)
+    GCG_GEMM_CASE(2, 1, 4, 1, 1)
+    GCG_GEMM_CASE(2, 2, 4, 1, 1)
+    GCG_GEMM_CASE(2, 3, 4, 1, 1)
+    GCG_GEMM_CASE(2, 4, 4, 1, 1)
+    GCG_GEMM_CASE(2, 5, 4, 1, 1)
+  } else {
+    GCG_GEMM_CASE(2, 1, 1, 4, 1)
+    GCG_GEMM_CASE(2, 4, 1, 4, 0)
+    GCG_GEMM_CASE(2, 2, 1, 4, 0)
+    GCG_GEMM_CASE(2, 3, 1, 4, 0)
+    GCG_GEMM_CASE(2, 4, 1, 4, 2)
+    GCG_GEMM_CASE(2, 3, 1, 4, 2)
+    GCG_GEMM_CASE(2, 2, 1, 4, 2)
+    GCG_GEMM_CASE(2, 4, 1, 4, 4)
+    GCG_GEMM_CASE(2, 4, 1, 4, 8)
+    GCG_GEMM_CASE(2, 4, 1, 4, 16)
+    GCG_GEMM_CASE(2, 3, 1, 4, 4)
+    GCG_GEMM_CASE(2, 2, 1, 4, 4)
+  }
 #undef GCG_GEMM_CASE
+#undef GCG_GEMM_BL_CASE
   return fail(GCG_ERR_INVALID_ARG, "gemm: no tile instantiated for RT=%d G=%d WR=%d WC=%d PF=%d",
               s.RT, s.G, s.WR, s.WC, s.PF);
 }
 
-// Tile choice. fused: the workgroup must hold the whole row (WC = 4, G = ceil(N/256)).
-// Plain: narrow N (<= 320) -> one wave spans all columns and 4 waves split 128 rows;
-// wider N -> row bands of 32 rows x up to 1024 columns, grid.y for the rest.
-Shape pick_shape(int64_t N, bool fused) {
+// Plain products (gcg_gemm). Tile 0, B through LDS (gemm_bl_kernel), measured on the train
+// step's shapes (tools/exp_gemm_bl.py, TFLOP/s, B-from-L2 gemm_kernel -> LDS-B):
+//   840k x 300 x 930  93.5 -> 96.7 (16 waves x 256 columns)   1.4M x 300 x 930  94.5 -> 97.0
+//   840k x 930 x 300  90.9 -> 105.1 (4 waves x 320 columns)   1.4M x 930 x 300  91.6 -> 105.7
+// Tile 1: B from L2 straight to registers (gemm_kernel), the same k order (bitwise equal).
+Shape pick_gemm_shape(int64_t N, int tile) {
   const int groups = static_cast<int>((N + 63) / 64);
-  // Wide (WC = 4) tiles, measured on Twitter-World's 840k x 300 x 930 (TFLOP/s, plain / fused):
-  //   RT = 4, B ping-pong, 1 workgroup per CU          92.8 / 78.7   <- plain default
-  //   RT = 2, B ping-pong, 1 workgroup per CU          83.0 / 72.2
-  //   RT = 2, one B set, 2 workgroups per CU           91.8 / 85.0-87.4: the second
-  //       workgroup hides B latency and overlaps the other's softmax epilogue + stores
-  //   ... + B set split into 2 / 4 / 8 / 16 rotating parts, groups past N skipped
-  //                                                    - / 92.3, 96.4, 96.8, 95.4
-  //                                                    <- fused default: 8 parts (PF = 8)
-  //   RT = 2, one B set, 8-wave workgroup              93.1 / 83.8
-  // Knobs for experiments: GCG_GEMM_RT=2, GCG_GEMM_8W=1, GCG_GEMM_OCC2=0/1,
-  // GCG_GEMM_SPLIT=0/2/4/8/16 (B parts of the 2-workgroup tiles).
-  const int rt = env_int("GCG_GEMM_RT") == 2 ? 2 : 4;
-  // Plain products: B through LDS (gemm_bl_kernel), measured on the train step's shapes
-  // (tools/exp_gemm_bl.py, TFLOP/s, B-from-L2 gemm_kernel -> LDS-B):
-  //   840k x 300 x 930  93.5 -> 96.7 (16 waves x 256 columns)   1.4M x 300 x 930  94.5 -> 97.0
-  //   840k x 930 x 300  90.9 -> 105.1 (4 waves x 320 columns)   1.4M x 930 x 300  91.6 -> 105.7
-  // The fused output layer keeps gemm_kernel: with one LDS-B workgroup per CU its softmax
-  // epilogue and 3 GB of gradient stores do not overlap another workgroup's MFMAs
-  // (77.9-79.3 vs 85.0 TFLOP/s). GCG_GEMM_BL=0 selects gemm_kernel for plain products too.
-  const char* blv = std::getenv("GCG_GEMM_BL");
-  if (!fused && !(blv && std::atoi(blv) == 0)) {
+  if (tile == 0) {
     if (groups <= 5) return Shape{1, std::max(groups, 1), 4, 1, 0, 1};
     if (groups <= 8) return Shape{1, 4, 4, 2, 0, 1};
     return Shape{1, 4, 4, 4, 0, 1};  // 1024 columns per workgroup, grid.y for the rest
   }
-  if (fused || groups > 5) {
-    const int g = std::min(4, (groups + 3) / 4);
-    if (env_int("GCG_GEMM_8W") && g == 4) return Shape{2, 4, 2, 4, 0};
-    const char* occ = std::getenv("GCG_GEMM_OCC2");
-    const bool occ2 = occ ? std::atoi(occ) != 0 : fused;
-    if (occ2 && g >= 2) {
-      const char* spv = std::getenv("GCG_GEMM_SPLIT");  // B ping-pong parts (0: none)
-      const int sp = spv ? std::atoi(spv) : 8;
-      const int np = sp >= 8 && g == 4 ? (sp >= 16 ? 16 : 8) : sp >= 4 ? 4 : sp >= 2 ? 2 : 0;
-      return Shape{2, g, 1, 4, np};
-    }
-    return Shape{g >= 2 ? rt : 2, std::max(g, 1), 1, 4};
-  }
-  return Shape{2, std::max(groups, 1), 4, 1};
+  if (groups <= 5) return Shape{2, std::max(groups, 1), 4, 1};  // one wave spans all columns
+  return Shape{4, std::min(4, (groups + 3) / 4), 1, 4};         // RT = 4, 1 workgroup per CU
+}
+
+// The fused output layer on the f32 MFMA (gemm_kernel EPI = 1): the workgroup holds the whole
+// row (WC = 4, G = ceil(N / 256)), measured on Twitter-World's 840k x 300 x 930 (TFLOP/s):
+//   RT = 4, B ping-pong, 1 workgroup per CU          78.7
+//   RT = 2, one B set, 2 workgroups per CU           85.0-87.4: the second workgroup hides B
+//       latency and overlaps the other's softmax epilogue + stores
+//   ... + B set split into 2 / 4 / 8 / 16 rotating parts, groups past N skipped
+//                                                    92.3, 96.4, 96.8, 95.4  <- 8 parts
+// `parts` (tiles 1..5: 0, 2, 4, 8, 16) only reorders MFMAs between distinct accumulators.
+constexpr int kFusedParts[] = {0, 2, 4, 8, 16};
+Shape pick_fused_shape(int64_t N, int parts) {
+  const int groups = static_cast<int>((N + 63) / 64);
+  const int g = std::min(4, (groups + 3) / 4);
+  if (g < 2) return Shape{2, 1, 1, 4};
+  const int sp = parts < 0 ? 8 : parts;
+  const int np = sp >= 8 && g == 4 ? (sp >= 16 ? 16 : 8) : sp >= 4 ? 4 : sp >= 2 ? 2 : 0;
+  return Shape{2, g, 1, 4, np};
 }
 
 gcg_status check_dense(const char* fn, const float* p, int64_t ld, int64_t cols, bool vec4) {
@@ -2029,23 +2096,31 @@ gcg_status check_dense(const char* fn, const float* p, int64_t ld, int64_t cols,
   return GCG_OK;
 }
 
-// The fused output layer on the bf16 matrix cores (gemm_fused6_kernel): 32 whole rows per
-// workgroup, G = ceil(N / 256) column groups per wave. GCG_FUSED_MATH=f32 keeps gemm_kernel.
-bool fused_bf16x6() {
-  const char* v = std::getenv("GCG_FUSED_MATH");
-  return !(v && std::strcmp(v, "f32") == 0);
+// Per-call arithmetic and tile: the math and tile arguments of the entry points.
+gcg_status check_opts(const char* fn, int op, int math, int tile) {
+  const int n = gcg_dense_tile_count(op, math);
+  if (n < 0) return fail(GCG_ERR_INVALID_ARG, "%s: math %d not available for this product", fn, math);
+  if (tile < 0 || tile > n)
+    return fail(GCG_ERR_INVALID_ARG, "%s: tile %d outside 0..%d", fn, tile, n);
+  return GCG_OK;
 }
+
+// The fused output layer on the bf16 matrix cores (gemm_fused6_kernel). ws != NULL: the weight's
+// planes pre-split into it (FX = 1); tile 0 = 64 rows x 8 waves of 128 columns at N > 768 (the
+// planes read once per 64 rows, half the 32-row form's L2 reads), else 32 rows x 4 waves; tile
+// 1 = the 32-row form at any N (bitwise the in-register split); tile 2 = the 64-row form (N >
+// 768 only). ws == NULL: the weight split in every workgroup's registers, 32 rows x 4 waves.
 gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, const float* B,
                          int64_t ldb, const float* bias, float* C, int64_t ldc,
                          const int32_t* labels, float scale, const float* scale_dev,
                          float* loss_rows, float* correct_rows, const float* row_w,
-                         hipStream_t st, void* ws = nullptr) {
+                         hipStream_t st, void* ws, int tile) {
   const int g = (N + 255) / 256;
   if (ws != nullptr) {  // the weight's planes pre-split (FX = 1) for the tile's BN columns
     const int Kc = (K + 31) / 32;
-    // N > 768: 64 rows x 8 waves of 128 columns (the weight's planes read once per 64 rows,
-    // half the 32-row form's L2 reads); GCG_FUSED6_FX_NARROW=1 keeps the 32-row 4-wave form
-    const bool wide = g == 4 && !env_int("GCG_FUSED6_FX_NARROW");
+    if (tile == 2 && g != 4)
+      return fail(GCG_ERR_INVALID_ARG, "fused layer: the 64-row tile needs N > 768 (N=%d)", N);
+    const bool wide = g == 4 && tile != 1;
     const int bn = wide ? 1024 : 256 * g;
     const int64_t threads = int64_t{bn} * Kc * 4;
     hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)),
@@ -2069,41 +2144,35 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
     GCG_HIP_CHECK(hipGetLastError());
     return GCG_OK;
   }
-  const int wr = env_int("GCG_FUSED6_WR") == 2 ? 2 : 1;  // experiment: 2 row bands (8 waves)
-  if (env_int("GCG_FUSED6_WIDE") && g == 4) {  // experiment: 64 rows x 8 waves of 128 columns
-    hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
-                       dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale,
-                       scale_dev, loss_rows, correct_rows, row_w);
-    GCG_HIP_CHECK(hipGetLastError());
-    return GCG_OK;
-  }
-  const dim3 grid(static_cast<unsigned>((M + 32 * wr - 1) / (32 * wr)));
-#define GCG_FUSED6_CASE(g_, wr_)                                                               \
-  if (g == g_ && wr == wr_) {                                                                 \
-    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_, wr_>), grid, dim3(256 * wr_), 0, st, int(M), \
-                       N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev,          \
-                       loss_rows, correct_rows, row_w);                                       \
+  if (tile != 0)
+    return fail(GCG_ERR_INVALID_ARG, "fused layer: tile %d needs the plane workspace", tile);
+  const dim3 grid(static_cast<unsigned>((M + 31) / 32));
+#define GCG_FUSED6_CASE(g_)                                                                    \
+  if (g == g_) {                                                                              \
+    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_, 1>), grid, dim3(256), 0, st, int(M), N, K, A, \
+                       lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows,        \
+                       correct_rows, row_w);                                                  \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
     return GCG_OK;                                                                            \
   }
-  GCG_FUSED6_CASE(1, 1)
-  GCG_FUSED6_CASE(2, 1)
-  GCG_FUSED6_CASE(3, 1)
-  GCG_FUSED6_CASE(4, 1)
-  GCG_FUSED6_CASE(1, 2)
-  GCG_FUSED6_CASE(2, 2)
-  GCG_FUSED6_CASE(3, 2)
-  GCG_FUSED6_CASE(4, 2)
+  GCG_FUSED6_CASE(1)
+  GCG_FUSED6_CASE(2)
+  GCG_FUSED6_CASE(3)
+  GCG_FUSED6_CASE(4)
 #undef GCG_FUSED6_CASE
   return fail(GCG_ERR_INVALID_ARG, "fused layer: N=%d", N);
 }
 
+// gcg_gemm / gcg_project_softmax_xent: validation, then the tile of (math, tile).
 gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t K,
                        const float* A, int64_t lda, const float* B, int64_t ldb,
                        const float* bias, int act, float* C, int64_t ldc,
                        const int32_t* labels, float scale, const float* scale_dev,
                        float* loss_rows, float* correct_rows, const float* row_w,
-                       gcg_stream_t stream, void* ws = nullptr) {
+                       gcg_stream_t stream, int math, int tile, void* ws = nullptr) {
+  gcg_status s;
+  if ((s = check_opts(fn, fused ? GCG_DENSE_FUSED : GCG_DENSE_GEMM, math, tile)) != GCG_OK)
+    return s;
   if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
                 static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
@@ -2112,7 +2181,6 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
                 static_cast<long long>(N));
   if (act != GCG_ACT_NONE && act != GCG_ACT_RELU)
     return fail(GCG_ERR_INVALID_ARG, "%s: unknown act %d", fn, act);
-  gcg_status s;
   if ((s = check_dense(fn, A, lda, K, true)) != GCG_OK) return s;
   // B is read as dwordx4 at columns < round4(N): its row stride must cover them.
   if ((s = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
@@ -2124,18 +2192,20 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
   if (row_w != nullptr && !aligned(row_w, 4))
     return fail(GCG_ERR_MISALIGNED, "%s: row_weight not 4-B aligned", fn);
   if (M == 0) return GCG_OK;
-  const Shape sh = pick_shape(N, fused);
-  // gemm_kernel reads B through a 32-bit buffer range (K * ldb * 4 bytes)
-  if (!sh.BL && K * ldb * 4 >= (int64_t{1} << 31))
+  // gemm_kernel / gemm_fused6_kernel read B through a 32-bit buffer range (K * ldb * 4 bytes)
+  if (K * ldb * 4 >= (int64_t{1} << 31))
     return fail(GCG_ERR_INVALID_ARG, "%s: B of %lld x %lld floats exceeds the 2 GB buffer range", fn,
                 static_cast<long long>(K), static_cast<long long>(ldb));
+  auto st = static_cast<hipStream_t>(stream);
+  if (fused && math == GCG_MATH_BF16X6) {
+    return launch_fused6(M, int(N), int(K), A, lda, B, ldb, bias, C, ldc, labels, scale,
+                         scale_dev, loss_rows, correct_rows, row_w, st, ws, tile);
+  }
+  const Shape sh = fused ? pick_fused_shape(N, tile == 0 ? -1 : kFusedParts[tile - 1])
+                         : pick_gemm_shape(N, tile);
   dim3 grid(static_cast<unsigned>((M + sh.bm() - 1) / sh.bm()),
             static_cast<unsigned>((N + sh.bn() - 1) / sh.bn()));
-  if (grid.x > 0x7fffffffu) return fail(GCG_ERR_INVALID_ARG, "%s: M too large", fn);
-  auto st = static_cast<hipStream_t>(stream);
-  if (fused && fused_bf16x6())
-    return launch_fused6(M, int(N), int(K), A, lda, B, ldb, bias, C, ldc, labels, scale,
-                         scale_dev, loss_rows, correct_rows, row_w, st, ws);
+  if ((M + sh.bm() - 1) / sh.bm() > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "%s: M too large", fn);
   if (fused)
     return launch_gemm<1>(sh, grid, st, int(M), int(N), int(K), A, lda, B, ldb, bias, act, C, ldc,
                           labels, scale, scale_dev, loss_rows, correct_rows, row_w);
@@ -2143,38 +2213,33 @@ gcg_status gemm_common(const char* fn, bool fused, int64_t M, int64_t N, int64_t
                         nullptr, 0.f, nullptr, nullptr, nullptr, nullptr);
 }
 
-// NT GEMM tile variants: (RT, G, WR, WC, S). Default BM = 256 x BN = 64, two stages,
-// two workgroups per CU (80 KB of LDS each); the others are experiment knobs (GCG_NT_CFG).
+// NT GEMM tiles on the f32 MFMA: (RT, G, WR, WC, S, PF, KC). Tile 0 = the first row.
 struct NtShape {
   int RT, G, WR, WC, S, PF = 0, KC = 32, MX = 0;
   int bm() const { return 16 * RT * WR; }
   int bn() const { return 64 * G * WC; }
 };
 
-// Measured on one MI355X (tools/exp_gemm_nt.py, TFLOP/s, hipBLASLt in brackets):
-//   840k x 300 x 930  (2,1,4,1,2,PF) 110.9-111.5  (2,1,4,1,3) 107  (4,1,4,1,2) 108   [100-104]
-//   840k x 930 x 300  (2,1,4,1,3,PF) 113.6-114.4  (2,1,4,1,2) 109  (4,1,4,1,2) 111-112 [110-111]
-//   450k x 300 x 256  (2,1,4,1,2) 109  [119];  450k x 256 x 300  (2,1,4,1,2) 108.6  [87]
-// BM = 128 x BN = 64 with 48-72 KB of LDS runs 2-3 workgroups per CU: one workgroup's
-// barrier, DMA wait and epilogue overlap the others' MFMAs. A deeper ring pays off on the
-// longer K loop (K = 930).
-// Round 2, later (K-tail zeroing moved to registers, occupancy hint from the LDS size):
-// 16-deep chunks in a 4-stage ring (2,1,4,1,4,KC=16): 48 KB, 3 workgroups per CU, three
-// chunks of DMA in flight: 118.0 / 118.0 / 114.4 / 111.2 on the four shapes above against
-// 108.6 / 113.3 / 112.2 / 109.9 for the 32-deep defaults (one box, mean of 10); 5-6 stages
-// (2 workgroups per CU) 104-113; 256 x 64 116 / 117.5; 128 x 128 91-115; 64 x 64 106-111;
-// 128 x 128 with 8 waves 115.0 / 101.2 / 118.9 / 95.9, 192 x 64 114.1 / 117.3 / 112.0 / 109.6
-// against 112.8 / 116.3 / 113.5 / 109.0 for the default on that box (not kept).
-NtShape pick_nt_shape(int64_t K) {
-  (void)K;
-  NtShape sh{2, 1, 4, 1, 4, 0, 16};
-  if (const char* v = std::getenv("GCG_NT_CFG")) {
-    int a = 0, b = 0, c = 0, d = 0, e = 0, f = 0, kc = 32;
-    const int n = std::sscanf(v, "%d,%d,%d,%d,%d,%d,%d", &a, &b, &c, &d, &e, &f, &kc);
-    if (n >= 5) sh = NtShape{a, b, c, d, e, n >= 6 ? f : 0, n == 7 ? kc : 32};
-  }
-  return sh;
-}
+// Measured on one MI355X (tools/exp_gemm_nt.py, TFLOP/s on 840k x 300 x 930 / 840k x 930 x 300
+// / 450k x 300 x 256 / 450k x 256 x 300): 16-deep chunks in a 4-stage ring (2,1,4,1,4,KC=16):
+// 48 KB, 3 workgroups per CU, three chunks of DMA in flight: 118.0 / 118.0 / 114.4 / 111.2
+// against 108.6 / 113.3 / 112.2 / 109.9 for the 32-deep 2-stage tile; 256 x 64 116 / 117.5;
+// 128 x 128 91-115; 64 x 64 106-111. BM = 128 x BN = 64 with 48-72 KB of LDS runs 2-3
+// workgroups per CU: one workgroup's barrier, DMA wait and epilogue overlap the others' MFMAs.
+constexpr NtShape kNtTiles[] = {
+    {2, 1, 4, 1, 4, 0, 16},  // 0: default, 128 x 64, 16-deep chunks, 4 stages
+    {2, 1, 4, 1, 2, 0, 32},  // 1: 32-deep chunks, 2 stages
+    {2, 1, 4, 1, 2, 1, 32},  // 2: ... both 16-deep steps' fragments read first
+    {2, 1, 4, 1, 3, 1, 32},  // 3: ... 3 stages
+    {4, 1, 4, 1, 2, 0, 32},  // 4: 256 x 64
+    {2, 2, 4, 1, 2, 0, 32},  // 5: 128 x 128
+    {2, 1, 2, 2, 2, 0, 32},  // 6: 2 x 2 waves
+    {2, 1, 4, 1, 3, 0, 16},  // 7: 16-deep, 3 stages
+    {4, 1, 4, 1, 4, 0, 16},  // 8: 256 x 64, 16-deep
+    {2, 2, 4, 1, 4, 0, 16},  // 9: 128 x 128, 16-deep
+    {1, 1, 4, 1, 4, 0, 16},  // 10: 64 x 64, 16-deep
+};
+constexpr int kNtTileCount = sizeof(kNtTiles) / sizeof(kNtTiles[0]) - 1;
 
 struct NtArgs {
   int M, N, K;
@@ -2194,8 +2259,8 @@ gcg_status launch_nt3_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
   hipLaunchKernelGGL((gemm_nt3_kernel<RT, G, WR, WC, S>), dim3(static_cast<unsigned>(rt * ct)),
-                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.bias, a.act, a.C,
-                     a.ldc, static_cast<int>(ct));
+                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                     a.act, a.C, a.ldc, static_cast<int>(ct));
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }
@@ -2206,8 +2271,8 @@ gcg_status launch_nt3r_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
   hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC>), dim3(static_cast<unsigned>(rt * ct)),
-                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.bias, a.act, a.C,
-                     a.ldc, static_cast<int>(ct));
+                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                     a.act, a.C, a.ldc, static_cast<int>(ct));
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }
@@ -2226,67 +2291,30 @@ gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
 }
 
 gcg_status launch_nt(const NtShape& sh, hipStream_t st, const NtArgs& a) {
-#define GCG_NTX_CASE(rt_, g_, wr_, wc_, s_)                                                     \
-  if (sh.MX == 1 && sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_)   \
-    return launch_nt_t<rt_, g_, wr_, wc_, s_, 1, 32, 1>(a, st);
-  GCG_NTX_CASE(2, 1, 4, 1, 2)
-  GCG_NTX_CASE(2, 1, 4, 1, 3)
-  GCG_NTX_CASE(4, 1, 4, 1, 2)
-  GCG_NTX_CASE(2, 2, 4, 1, 2)
-  GCG_NTX_CASE(2, 1, 2, 2, 2)
-#undef GCG_NTX_CASE
-  if (sh.MX != 0)
-    return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt: no bf16x6 tile RT=%d G=%d WR=%d WC=%d S=%d",
-                sh.RT, sh.G, sh.WR, sh.WC, sh.S);
-#define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_)                                                  \
+  // bf16x6 with both operands split in the loop (no workspace): 128 x 64, 32-deep, 2 stages
+  if (sh.MX == 1) return launch_nt_t<2, 1, 4, 1, 2, 1, 32, 1>(a, st);
+#define GCG_NT_CASE(rt_, g_, wr_, wc_, s_, pf_, kc_)                                             \
   if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_ && sh.PF == pf_ && \
-      sh.KC == 32)                                                                               \
-    return launch_nt_t<rt_, g_, wr_, wc_, s_, pf_, 32>(a, st);
-  GCG_NT_CASE(2, 1, 4, 1, 2, 0)
-  GCG_NT_CASE(2, 1, 4, 1, 2, 1)
-  GCG_NT_CASE(2, 1, 4, 1, 3, 0)
-  GCG_NT_CASE(2, 1, 4, 1, 3, 1)
-  GCG_NT_CASE(1, 1, 4, 1, 2, 0)
-  GCG_NT_CASE(1, 1, 4, 1, 3, 0)
-  GCG_NT_CASE(3, 1, 4, 1, 2, 0)
-  GCG_NT_CASE(2, 2, 4, 1, 2, 0)
-  GCG_NT_CASE(2, 1, 2, 2, 2, 0)
-  GCG_NT_CASE(4, 1, 4, 1, 2, 0)
+      sh.KC == kc_)                                                                              \
+    return launch_nt_t<rt_, g_, wr_, wc_, s_, pf_, kc_>(a, st);
+  GCG_NT_CASE(2, 1, 4, 1, 4, 0, 16)
+  GCG_NT_CASE(2, 1, 4, 1, 2, 0, 32)
+  GCG_NT_CASE(2, 1, 4, 1, 2, 1, 32)
+  GCG_NT_CASE(2, 1, 4, 1, 3, 1, 32)
+  GCG_NT_CASE(4, 1, 4, 1, 2, 0, 32)
+  GCG_NT_CASE(2, 2, 4, 1, 2, 0, 32)
+  GCG_NT_CASE(2, 1, 2, 2, 2, 0, 32)
+  GCG_NT_CASE(2, 1, 4, 1, 3, 0, 16)
+  GCG_NT_CASE(4, 1, 4, 1, 4, 0, 16)
+  GCG_NT_CASE(2, 2, 4, 1, 4, 0, 16)
+  GCG_NT_CASE(1, 1, 4, 1, 4, 0, 16)
 #undef GCG_NT_CASE
-#define GCG_NT16_CASE(rt_, g_, s_)                                                              \
-  if (sh.KC == 16 && sh.RT == rt_ && sh.G == g_ && sh.WR == 4 && sh.WC == 1 && sh.S == s_)      \
-    return launch_nt_t<rt_, g_, 4, 1, s_, 0, 16>(a, st);
-  GCG_NT16_CASE(2, 1, 2)
-  GCG_NT16_CASE(2, 1, 3)
-  GCG_NT16_CASE(2, 1, 4)
-  GCG_NT16_CASE(2, 1, 5)
-  GCG_NT16_CASE(2, 1, 6)
-  GCG_NT16_CASE(4, 1, 4)
-  GCG_NT16_CASE(2, 2, 4)
-  GCG_NT16_CASE(1, 1, 4)
-  GCG_NT16_CASE(1, 1, 6)
-#undef GCG_NT16_CASE
-  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32: no tile RT=%d G=%d WR=%d WC=%d S=%d PF=%d KC=%d",
+  return fail(GCG_ERR_INVALID_ARG, "gemm_nt: no tile RT=%d G=%d WR=%d WC=%d S=%d PF=%d KC=%d",
               sh.RT, sh.G, sh.WR, sh.WC, sh.S, sh.PF, sh.KC);
 }
 
-// bf16x6 tiles (MX = 1; 32-deep chunks): default 128 x 64, two stages; GCG_NTX_CFG =
-// "RT,G,WR,WC,S" picks another (experiment knob).
-NtShape pick_ntx_shape() {
-  NtShape sh{2, 1, 4, 1, 2, 1, 32, 1};
-  if (const char* v = std::getenv("GCG_NTX_CFG")) {
-    int a = 0, b = 0, c = 0, d = 0, e = 0;
-    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) == 5) sh = NtShape{a, b, c, d, e, 1, 32, 1};
-  }
-  return sh;
-}
-
-gcg_status gemm_nt_common(const char* fn, int mx, int64_t M, int64_t N, int64_t K, const float* A,
-                          int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int act,
-                          float* C, int64_t ldc, gcg_stream_t stream);
-
-// pre-split bf16x6 tiles (gemm_nt3_kernel): default 128 x 64, two stages; GCG_NT3_CFG =
-// "RT,G,WR,WC,S" picks another (experiment knob; S = 0: gemm_nt3r_kernel, A in registers).
+// bf16x6 NT tiles with the weight's planes pre-split: (RT, G, WR, WC, S); S = 0:
+// gemm_nt3r_kernel (A in registers), S = 2: gemm_nt3_kernel (A through the LDS-DMA ring).
 struct Nt3Shape {
   int RT, G, WR, WC, S;
 };
@@ -2297,8 +2325,7 @@ struct Nt3Shape {
 //   1.4M x 300 x 930           146          151-152     154-155  |             165-166  171      151
 //   450k x 300 x 256           138-141      155         154-155  |             155-157  168-170  141-142
 //   450k x 256 x 300           136          138-139     134-137  |             143-145  142      129
-// (deeper rings, S = 3, lost 15-30: one workgroup per CU). Default: register A, 128 rows x
-// 64 G columns, G in 1..3 (the register-A rows of the table above are G = 1 / 2):
+// Default: register A, 128 rows x 64 G columns, G in 1..3:
 //                       G = 1      G = 2      G = 3
 //   840k x 300 x 930    166-168    171-173    175-176   (N padded to 960 / 1024 / 960)
 //   840k x 930 x 300    162-163    166        170-172   (320 / 384 / 384)
@@ -2306,6 +2333,18 @@ struct Nt3Shape {
 //   450k x 256 x 300    144.5      142-144    137-138   (320 / 384 / 384)
 // Rule: the G padding N least (ties: the larger G -- fewer re-reads of A); for K > 512 the
 // largest G within 1.25 x the least padding (a long k loop amortises the wider tile's waste).
+constexpr Nt3Shape kNt3Tiles[] = {
+    {2, 1, 4, 1, 0},  // 1: register A, 128 x 64
+    {2, 2, 4, 1, 0},  // 2: register A, 128 x 128
+    {2, 3, 4, 1, 0},  // 3: register A, 128 x 192
+    {4, 1, 4, 1, 0},  // 4: register A, 256 x 64
+    {2, 1, 4, 1, 2},  // 5: LDS A, 128 x 64
+    {2, 2, 4, 1, 2},  // 6: LDS A, 128 x 128
+    {2, 1, 4, 2, 2},  // 7: LDS A, 2 column waves
+    {4, 1, 4, 1, 2},  // 8: LDS A, 256 x 64
+};
+constexpr int kNt3TileCount = sizeof(kNt3Tiles) / sizeof(kNt3Tiles[0]);
+
 Nt3Shape pick_nt3_shape(int64_t N, int64_t K) {
   int64_t pad[4] = {0, 0, 0, 0}, least = INT64_MAX;
   for (int g = 1; g <= 3; ++g) {
@@ -2315,28 +2354,16 @@ Nt3Shape pick_nt3_shape(int64_t N, int64_t K) {
   int best = 1;
   for (int g = 1; g <= 3; ++g)
     if (pad[g] == least || (K > 512 && 4 * pad[g] <= 5 * least)) best = g;
-  Nt3Shape sh{2, best, 4, 1, 0};
-  if (const char* v = std::getenv("GCG_NT3_CFG")) {
-    int a = 0, b = 0, c = 0, d = 0, e = 0;
-    if (std::sscanf(v, "%d,%d,%d,%d,%d", &a, &b, &c, &d, &e) == 5) sh = Nt3Shape{a, b, c, d, e};
-  }
-  return sh;
+  return Nt3Shape{2, best, 4, 1, 0};
 }
 gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const unsigned* Bs) {
 #define GCG_NT3_CASE(rt_, g_, wr_, wc_, s_)                                                    \
   if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == s_)                \
     return launch_nt3_t<rt_, g_, wr_, wc_, s_>(a, Bs, st);
   GCG_NT3_CASE(2, 1, 4, 1, 2)
-  GCG_NT3_CASE(2, 1, 4, 1, 3)
-  GCG_NT3_CASE(4, 1, 4, 1, 2)
   GCG_NT3_CASE(2, 2, 4, 1, 2)
-  GCG_NT3_CASE(2, 2, 4, 1, 3)
-  GCG_NT3_CASE(2, 1, 2, 2, 2)
-  GCG_NT3_CASE(4, 1, 2, 2, 2)
   GCG_NT3_CASE(2, 1, 4, 2, 2)
-  GCG_NT3_CASE(2, 1, 4, 2, 3)
-  GCG_NT3_CASE(2, 2, 4, 2, 2)
-  GCG_NT3_CASE(4, 1, 4, 2, 2)
+  GCG_NT3_CASE(4, 1, 4, 1, 2)
 #undef GCG_NT3_CASE
 #define GCG_NT3R_CASE(rt_, g_, wr_, wc_)                                                       \
   if (sh.RT == rt_ && sh.G == g_ && sh.WR == wr_ && sh.WC == wc_ && sh.S == 0)                 \
@@ -2344,25 +2371,158 @@ gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const
   GCG_NT3R_CASE(2, 1, 4, 1)
   GCG_NT3R_CASE(2, 2, 4, 1)
   GCG_NT3R_CASE(2, 3, 4, 1)
-  GCG_NT3R_CASE(2, 3, 2, 1)
   GCG_NT3R_CASE(4, 1, 4, 1)
-  GCG_NT3R_CASE(2, 1, 2, 1)
-  GCG_NT3R_CASE(2, 2, 2, 1)
-  GCG_NT3R_CASE(4, 1, 2, 1)
-  GCG_NT3R_CASE(2, 1, 4, 2)
 #undef GCG_NT3R_CASE
-  return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_nt_f32_bf16x6: no tile RT=%d G=%d WR=%d WC=%d S=%d",
+  return fail(GCG_ERR_INVALID_ARG, "gemm_nt bf16x6: no tile RT=%d G=%d WR=%d WC=%d S=%d",
               sh.RT, sh.G, sh.WR, sh.WC, sh.S);
+}
+
+gcg_status gemm_nt_impl(const char* fn, int64_t M, int64_t N, int64_t K, const float* A,
+                        int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int act,
+                        float* C, int64_t ldc, int math, int tile, void* ws, int64_t ws_bytes,
+                        gcg_stream_t stream) {
+  gcg_status s;
+  if ((s = check_opts(fn, GCG_DENSE_GEMM_NT, math, tile)) != GCG_OK) return s;
+  if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
+                static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
+  if (act != GCG_ACT_NONE && act != GCG_ACT_RELU)
+    return fail(GCG_ERR_INVALID_ARG, "%s: unknown act %d", fn, act);
+  // both operands are read as 16-B k-segments up to round4(K)
+  if ((s = check_dense(fn, A, lda, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
+  if ((s = check_dense(fn, Bt, ldbt, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
+  if ((s = check_dense(fn, C, ldc, N, true)) != GCG_OK) return s;
+  if (bias != nullptr && !aligned(bias, 4)) return fail(GCG_ERR_MISALIGNED, "%s: bias", fn);
+  NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  if (math == GCG_MATH_F32) {
+    if (M == 0) return GCG_OK;
+    return launch_nt(kNtTiles[tile], st, a);
+  }
+  // bf16x6. Planes or A tiles past the 32-bit buffer offsets: both operands split in the loop.
+  if (ws != nullptr && (gcg_gemm_nt_bf16x6_workspace(N, K) > INT32_MAX || 256 * lda * 4 > INT32_MAX / 2)) {
+    if (tile != 0) return fail(GCG_ERR_INVALID_ARG, "%s: operands too large for tile %d", fn, tile);
+    ws = nullptr;
+  }
+  if (ws == nullptr) {
+    if (tile != 0) return fail(GCG_ERR_INVALID_ARG, "%s: tile %d needs the plane workspace", fn, tile);
+    if (M == 0) return GCG_OK;
+    NtShape sh{};
+    sh.MX = 1;
+    return launch_nt(sh, st, a);
+  }
+  if (ws_bytes < gcg_gemm_nt_bf16x6_workspace(N, K))
+    return fail(GCG_ERR_WORKSPACE, "%s: workspace %lld B < %lld B", fn,
+                static_cast<long long>(ws_bytes),
+                static_cast<long long>(gcg_gemm_nt_bf16x6_workspace(N, K)));
+  if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
+  if (M == 0) return GCG_OK;
+  const int Kc = static_cast<int>((K + 31) / 32);
+  const int64_t threads = N * Kc * 4;
+  hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256),
+                     0, st, int(N), int(K), Kc, Bt, ldbt, static_cast<unsigned*>(ws));
+  GCG_HIP_CHECK(hipGetLastError());
+  return launch_nt3(tile == 0 ? pick_nt3_shape(N, K) : kNt3Tiles[tile - 1], st, a,
+                    static_cast<const unsigned*>(ws));
+}
+
+gcg_status gemm_tn_impl(const char* fn, int64_t R, int64_t M, int64_t N, const float* A,
+                        int64_t lda, const float* B, int64_t ldb, const float* scale_dev,
+                        float* C, int64_t ldc, int math, int tile, void* workspace,
+                        size_t workspace_bytes, gcg_stream_t stream) {
+  gcg_status st;
+  if ((st = check_opts(fn, GCG_DENSE_GEMM_TN, math, tile)) != GCG_OK) return st;
+  if (R < 0 || M <= 0 || N <= 0 || R > INT32_MAX || M > INT32_MAX || N > INT32_MAX)
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes R=%lld M=%lld N=%lld", fn,
+                static_cast<long long>(R), static_cast<long long>(M), static_cast<long long>(N));
+  // dwordx4 row reads at columns < round4(M) / round4(N)
+  if ((st = check_dense(fn, A, lda, (M + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
+  if ((st = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
+  if ((st = check_dense(fn, C, ldc, N, false)) != GCG_OK) return st;
+  if (lda >= (int64_t{1} << 27) || ldb >= (int64_t{1} << 27))  // 4-row buffer ranges < 2 GB
+    return fail(GCG_ERR_INVALID_ARG, "%s: leading dimension too large", fn);
+  auto s = static_cast<hipStream_t>(stream);
+  if (R == 0) {
+    for (int64_t m = 0; m < M; ++m)
+      GCG_HIP_CHECK(hipMemsetAsync(C + m * ldc, 0, sizeof(float) * N, s));
+    return GCG_OK;
+  }
+  const TnPlan p = tn_plan(R, M, N, tile);
+  const size_t need = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
+  if (workspace == nullptr || workspace_bytes < need)
+    return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu bytes < %zu needed", fn, workspace_bytes,
+                need);
+  if (!aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace not 16-B aligned", fn);
+  float* part = static_cast<float*>(workspace);
+  int64_t n_tiles = int64_t{p.mt} * p.nt * p.S;
+  if (n_tiles > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "%s: too many tiles", fn);
+  if (p.wm == 0) n_tiles = (n_tiles + 3) / 4;  // 4 wave tiles per workgroup
+  const dim3 grid(static_cast<unsigned>(n_tiles));
+  constexpr int remap = 1;  // XCD-aware tile order (+1-3 % dW2, +14 % X head)
+#define GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, OCC_)                                            \
+  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_ && p.occ == OCC_) {           \
+    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_, OCC_>), grid,             \
+                       dim3(WM_ <= 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
+                       B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);       \
+  } else
+#define GCG_TN_CASE(MG_, NG_, PD_, WM_) GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, 0)
+  GCG_TN_CASE(1, 2, 8, 1)
+  GCG_TN_CASE(1, 1, 8, 1)
+  GCG_TN_CASE(1, 1, 8, 2)
+  GCG_TN_CASE(1, 1, 8, 3)
+  GCG_TN_CASE(1, 1, 8, 4)
+  GCG_TN_CASE(1, 2, 8, 0)
+  GCG_TN_CASE(1, 3, 8, 0)
+  GCG_TN_CASE(1, 3, 12, 0)
+  GCG_TN_CASE_OCC(1, 3, 3, 0, 2)
+  GCG_TN_CASE_OCC(1, 2, 6, 0, 2)
+  { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d WM=%d OCC=%d", fn, p.mg,
+                p.ng, p.pd, p.wm, p.occ); }
+#undef GCG_TN_CASE
+#undef GCG_TN_CASE_OCC
+  GCG_HIP_CHECK(hipGetLastError());
+  const int vec = (ldc % 4 == 0 && aligned(C, 16)) ? 1 : 0;
+  const dim3 rgrid(static_cast<unsigned>(((N + 3) / 4 + 63) / 64),
+                   static_cast<unsigned>(std::min<int64_t>(M, 65535)));
+  hipLaunchKernelGGL(gemm_tn_reduce_kernel, rgrid, dim3(64 * kTnRedWaves), 0, s, int(M), int(N),
+                     p.S, part, p.Mp, p.Np, scale_dev, C, ldc, vec);
+  GCG_HIP_CHECK(hipGetLastError());
+  return GCG_OK;
 }
 
 }  // namespace
 
 extern "C" {
 
+int32_t gcg_dense_tile_count(int32_t op, int32_t math) {
+  switch (op) {
+    case GCG_DENSE_GEMM: return math == GCG_MATH_F32 ? 1 : -1;
+    case GCG_DENSE_GEMM_NT:
+      return math == GCG_MATH_F32 ? kNtTileCount : math == GCG_MATH_BF16X6 ? kNt3TileCount : -1;
+    case GCG_DENSE_FUSED:
+      return math == GCG_MATH_F32 ? 5 : math == GCG_MATH_BF16X6 ? 2 : -1;
+    case GCG_DENSE_GEMM_TN: return math == GCG_MATH_F32 ? kTnTileCount : -1;
+    default: return -1;
+  }
+}
+
+gcg_status gcg_gemm_nt(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                       const float* Bt, int64_t ldbt, const float* bias, int act, float* C,
+                       int64_t ldc, int32_t math, int32_t tile, void* ws, int64_t ws_bytes,
+                       gcg_stream_t stream) {
+  return gemm_nt_impl("gcg_gemm_nt", M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, math, tile, ws,
+                      ws_bytes, stream);
+}
+
+int64_t gcg_gemm_nt_workspace(int64_t N, int64_t K, int32_t math) {
+  return math == GCG_MATH_BF16X6 ? gcg_gemm_nt_bf16x6_workspace(N, K) : 0;
+}
+
 gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                            const float* Bt, int64_t ldbt, const float* bias, int act, float* C,
                            int64_t ldc, gcg_stream_t stream) {
-  return gemm_nt_common("gcg_gemm_nt_f32", 0, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
+  return gemm_nt_impl("gcg_gemm_nt_f32", M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc,
+                      GCG_MATH_F32, 0, nullptr, 0, stream);
 }
 
 int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K) {
@@ -2374,63 +2534,53 @@ gcg_status gcg_gemm_nt_f32_bf16x6(int64_t M, int64_t N, int64_t K, const float* 
                                   const float* Bt, int64_t ldbt, const float* bias, int act,
                                   float* C, int64_t ldc, void* ws, int64_t ws_bytes,
                                   gcg_stream_t stream) {
-  const char* fn = "gcg_gemm_nt_f32_bf16x6";
-  // no workspace, or planes / A tiles past the 32-bit buffer offsets: both operands split in
-  // the loop (gemm_nt_kernel MX = 1)
-  if (ws != nullptr && (gcg_gemm_nt_bf16x6_workspace(N, K) > INT32_MAX || 256 * lda * 4 > INT32_MAX / 2))
-    ws = nullptr;
-  if (ws == nullptr)
-    return gemm_nt_common(fn, 1, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
-  if (ws_bytes < gcg_gemm_nt_bf16x6_workspace(N, K))
-    return fail(GCG_ERR_INVALID_ARG, "%s: workspace %lld B < %lld B", fn,
-                static_cast<long long>(ws_bytes),
-                static_cast<long long>(gcg_gemm_nt_bf16x6_workspace(N, K)));
-  if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
-  gcg_status s = gemm_nt_common(fn, 2, M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc, stream);
-  if (s != GCG_OK || M == 0) return s;
-  const int Kc = static_cast<int>((K + 31) / 32);
-  const int64_t threads = N * Kc * 4;
-  hipStream_t st = static_cast<hipStream_t>(stream);
-  hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256),
-                     0, st, int(N), int(K), Kc, Bt, ldbt, static_cast<unsigned*>(ws));
-  GCG_HIP_CHECK(hipGetLastError());
-  NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
-  return launch_nt3(pick_nt3_shape(N, K), st, a, static_cast<const unsigned*>(ws));
+  return gemm_nt_impl("gcg_gemm_nt_f32_bf16x6", M, N, K, A, lda, Bt, ldbt, bias, act, C, ldc,
+                      GCG_MATH_BF16X6, 0, ws, ws_bytes, stream);
 }
 
-}  // extern "C"
-
-namespace {
-
-gcg_status gemm_nt_common(const char* fn, int mx, int64_t M, int64_t N, int64_t K, const float* A,
-                          int64_t lda, const float* Bt, int64_t ldbt, const float* bias, int act,
-                          float* C, int64_t ldc, gcg_stream_t stream) {
-  if (M < 0 || N <= 0 || K <= 0 || M > INT32_MAX || N > INT32_MAX || K > INT32_MAX)
-    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes M=%lld N=%lld K=%lld", fn,
-                static_cast<long long>(M), static_cast<long long>(N), static_cast<long long>(K));
-  if (act != GCG_ACT_NONE && act != GCG_ACT_RELU)
-    return fail(GCG_ERR_INVALID_ARG, "%s: unknown act %d", fn, act);
-  gcg_status s;
-  // both operands are read as 16-B k-segments up to round4(K)
-  if ((s = check_dense(fn, A, lda, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
-  if ((s = check_dense(fn, Bt, ldbt, (K + 3) & ~int64_t{3}, true)) != GCG_OK) return s;
-  if ((s = check_dense(fn, C, ldc, N, true)) != GCG_OK) return s;
-  if (bias != nullptr && !aligned(bias, 4)) return fail(GCG_ERR_MISALIGNED, "%s: bias", fn);
-  if (M == 0) return GCG_OK;
-  if (mx == 2) return GCG_OK;  // validation only (the pre-split path launches itself)
-  NtArgs a{int(M), int(N), int(K), A, lda, Bt, ldbt, bias, act, C, ldc};
-  return launch_nt(mx ? pick_ntx_shape() : pick_nt_shape(K), static_cast<hipStream_t>(stream), a);
+gcg_status gcg_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                    int64_t ldb, const float* bias, int act, float* C, int64_t ldc, int32_t math,
+                    int32_t tile, gcg_stream_t stream) {
+  return gemm_common("gcg_gemm", false, M, N, K, A, lda, B, ldb, bias, act, C, ldc, nullptr,
+                     0.f, nullptr, nullptr, nullptr, nullptr, stream, math, tile);
 }
-
-}  // namespace
-
-extern "C" {
 
 gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         const float* B, int64_t ldb, const float* bias, int act, float* C,
                         int64_t ldc, gcg_stream_t stream) {
   return gemm_common("gcg_gemm_f32", false, M, N, K, A, lda, B, ldb, bias, act, C, ldc, nullptr,
-                     0.f, nullptr, nullptr, nullptr, nullptr, stream);
+                     0.f, nullptr, nullptr, nullptr, nullptr, stream, GCG_MATH_F32, 0);
+}
+
+int64_t gcg_project_softmax_xent_workspace(int64_t N, int64_t K, int32_t math) {
+  if (math != GCG_MATH_BF16X6 || N <= 0 || N > 1024 || K <= 0) return 0;
+  return int64_t{1024} * ((K + 31) / 32) * 192;
+}
+
+int64_t gcg_project_softmax_xent_bf16x6_workspace(int64_t N, int64_t K) {
+  return gcg_project_softmax_xent_workspace(N, K, GCG_MATH_BF16X6);
+}
+
+gcg_status gcg_project_softmax_xent(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                    const float* W, int64_t ldw, const float* bias,
+                                    const int32_t* labels, float scale, const float* scale_dev,
+                                    float* out, int64_t ldo, float* loss_rows,
+                                    float* correct_rows, const float* row_weight, int32_t math,
+                                    int32_t tile, void* ws, int64_t ws_bytes,
+                                    gcg_stream_t stream) {
+  const char* fn = "gcg_project_softmax_xent";
+  if (math == GCG_MATH_BF16X6 && ws != nullptr) {
+    if (ws_bytes < gcg_project_softmax_xent_workspace(N, K, math))
+      return fail(GCG_ERR_WORKSPACE, "%s: workspace %lld B too small", fn,
+                  static_cast<long long>(ws_bytes));
+    if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
+    if (int64_t{1024} * ((K + 31) / 32) * 192 > INT32_MAX) {  // 32-bit plane offsets
+      if (tile != 0) return fail(GCG_ERR_INVALID_ARG, "%s: K too large for tile %d", fn, tile);
+      ws = nullptr;
+    }
+  }
+  return gemm_common(fn, true, M, N, K, A, lda, W, ldw, bias, GCG_ACT_NONE, out, ldo, labels,
+                     scale, scale_dev, loss_rows, correct_rows, row_weight, stream, math, tile, ws);
 }
 
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
@@ -2441,7 +2591,7 @@ gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const f
                                         gcg_stream_t stream) {
   return gemm_common("gcg_project_softmax_xent_f32", true, M, N, K, A, lda, W, ldw, bias,
                      GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows, correct_rows,
-                     nullptr, stream);
+                     nullptr, stream, GCG_MATH_F32, 0);
 }
 
 gcg_status gcg_project_softmax_xent_weighted_f32(int64_t M, int64_t N, int64_t K,
@@ -2454,12 +2604,7 @@ gcg_status gcg_project_softmax_xent_weighted_f32(int64_t M, int64_t N, int64_t K
                                                  gcg_stream_t stream) {
   return gemm_common("gcg_project_softmax_xent_weighted_f32", true, M, N, K, A, lda, W, ldw,
                      bias, GCG_ACT_NONE, out, ldo, labels, scale, scale_dev, loss_rows,
-                     correct_rows, row_weight, stream);
-}
-
-int64_t gcg_project_softmax_xent_bf16x6_workspace(int64_t N, int64_t K) {
-  if (N <= 0 || N > 1024 || K <= 0) return 0;
-  return int64_t{1024} * ((K + 31) / 32) * 192;
+                     correct_rows, row_weight, stream, GCG_MATH_F32, 0);
 }
 
 gcg_status gcg_project_softmax_xent_weighted_ws_f32(
@@ -2467,16 +2612,9 @@ gcg_status gcg_project_softmax_xent_weighted_ws_f32(
     const float* bias, const int32_t* labels, float scale, const float* scale_dev, float* out,
     int64_t ldo, float* loss_rows, float* correct_rows, const float* row_weight, void* ws,
     int64_t ws_bytes, gcg_stream_t stream) {
-  const char* fn = "gcg_project_softmax_xent_weighted_ws_f32";
-  if (ws != nullptr) {
-    if (ws_bytes < gcg_project_softmax_xent_bf16x6_workspace(N, K))
-      return fail(GCG_ERR_INVALID_ARG, "%s: workspace %lld B too small", fn,
-                  static_cast<long long>(ws_bytes));
-    if (!aligned(ws, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace", fn);
-    if (int64_t{1024} * ((K + 31) / 32) * 192 > INT32_MAX) ws = nullptr;  // 32-bit offsets
-  }
-  return gemm_common(fn, true, M, N, K, A, lda, W, ldw, bias, GCG_ACT_NONE, out, ldo, labels,
-                     scale, scale_dev, loss_rows, correct_rows, row_weight, stream, ws);
+  return gcg_project_softmax_xent(M, N, K, A, lda, W, ldw, bias, labels, scale, scale_dev, out,
+                                  ldo, loss_rows, correct_rows, row_weight, GCG_MATH_BF16X6, 0, ws,
+                                  ws_bytes, stream);
 }
 
 gcg_status gcg_softmax_xent_f32(int64_t M, int64_t N, const float* logits, int64_t ldl,
@@ -2526,87 +2664,38 @@ gcg_status gcg_softmax_xent_weighted_f32(int64_t M, int64_t N, const float* logi
   return fail(GCG_ERR_INVALID_ARG, "%s: N too large", fn);
 }
 
-gcg_status gcg_gemm_tn_f32_workspace_bytes(int64_t R, int64_t M, int64_t N, size_t* bytes) {
+gcg_status gcg_gemm_tn_workspace_bytes(int64_t R, int64_t M, int64_t N, int32_t math,
+                                       int32_t tile, size_t* bytes) {
+  const char* fn = "gcg_gemm_tn_workspace_bytes";
+  gcg_status s;
+  if ((s = check_opts(fn, GCG_DENSE_GEMM_TN, math, tile)) != GCG_OK) return s;
   if (R < 0 || M <= 0 || N <= 0 || R > INT32_MAX || M > INT32_MAX || N > INT32_MAX ||
       bytes == nullptr)
-    return fail(GCG_ERR_INVALID_ARG, "gcg_gemm_tn_f32_workspace_bytes: bad sizes");
+    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes", fn);
   if (R == 0) { *bytes = 0; return GCG_OK; }
-  const TnPlan p = tn_plan(R, M, N);
+  const TnPlan p = tn_plan(R, M, N, tile);
   *bytes = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
   return GCG_OK;
+}
+
+gcg_status gcg_gemm_tn_f32_workspace_bytes(int64_t R, int64_t M, int64_t N, size_t* bytes) {
+  return gcg_gemm_tn_workspace_bytes(R, M, N, GCG_MATH_F32, 0, bytes);
+}
+
+gcg_status gcg_gemm_tn(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
+                       const float* B, int64_t ldb, const float* scale_dev, float* C, int64_t ldc,
+                       int32_t math, int32_t tile, void* workspace, size_t workspace_bytes,
+                       gcg_stream_t stream) {
+  return gemm_tn_impl("gcg_gemm_tn", R, M, N, A, lda, B, ldb, scale_dev, C, ldc, math, tile,
+                      workspace, workspace_bytes, stream);
 }
 
 gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
                            const float* B, int64_t ldb, const float* scale_dev, float* C,
                            int64_t ldc, void* workspace, size_t workspace_bytes,
                            gcg_stream_t stream) {
-  const char* fn = "gcg_gemm_tn_f32";
-  if (R < 0 || M <= 0 || N <= 0 || R > INT32_MAX || M > INT32_MAX || N > INT32_MAX)
-    return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes R=%lld M=%lld N=%lld", fn,
-                static_cast<long long>(R), static_cast<long long>(M), static_cast<long long>(N));
-  gcg_status st;
-  // dwordx4 row reads at columns < round4(M) / round4(N)
-  if ((st = check_dense(fn, A, lda, (M + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
-  if ((st = check_dense(fn, B, ldb, (N + 3) & ~int64_t{3}, true)) != GCG_OK) return st;
-  if ((st = check_dense(fn, C, ldc, N, false)) != GCG_OK) return st;
-  if (lda >= (int64_t{1} << 27) || ldb >= (int64_t{1} << 27))  // 4-row buffer ranges < 2 GB
-    return fail(GCG_ERR_INVALID_ARG, "%s: leading dimension too large", fn);
-  auto s = static_cast<hipStream_t>(stream);
-  if (R == 0) {
-    for (int64_t m = 0; m < M; ++m)
-      GCG_HIP_CHECK(hipMemsetAsync(C + m * ldc, 0, sizeof(float) * N, s));
-    return GCG_OK;
-  }
-  const TnPlan p = tn_plan(R, M, N);
-  const size_t need = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
-  if (workspace == nullptr || workspace_bytes < need)
-    return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu bytes < %zu needed", fn, workspace_bytes,
-                need);
-  if (!aligned(workspace, 16)) return fail(GCG_ERR_MISALIGNED, "%s: workspace not 16-B aligned", fn);
-  float* part = static_cast<float*>(workspace);
-  int64_t n_tiles = int64_t{p.mt} * p.nt * p.S;
-  if (n_tiles > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "%s: too many tiles", fn);
-  if (p.wm == 0) n_tiles = (n_tiles + 3) / 4;  // 4 wave tiles per workgroup
-  const dim3 grid(static_cast<unsigned>(n_tiles));
-  const char* rmv = std::getenv("GCG_TN_XCD");  // experiment knob: 0 = hardware order
-  const int remap = rmv ? std::atoi(rmv) : 1;
-#define GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, OCC_)                                            \
-  if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_ && p.occ == OCC_) {           \
-    hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_, OCC_>), grid,             \
-                       dim3(WM_ <= 1 ? 256 : 64 * WM_), 0, s, int(R), int(M), int(N), A, lda, \
-                       B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt, remap);       \
-  } else
-#define GCG_TN_CASE(MG_, NG_, PD_, WM_) GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, 0)
-  GCG_TN_CASE(1, 2, 4, 1)
-  GCG_TN_CASE(1, 2, 8, 1)
-  GCG_TN_CASE(1, 1, 8, 1)
-  GCG_TN_CASE(1, 1, 16, 1)
-  GCG_TN_CASE(1, 2, 8, 4)
-  GCG_TN_CASE(1, 2, 8, 5)
-  GCG_TN_CASE(1, 1, 8, 2)
-  GCG_TN_CASE(1, 1, 8, 3)
-  GCG_TN_CASE(1, 1, 8, 4)
-  GCG_TN_CASE(1, 1, 8, 5)
-  GCG_TN_CASE(1, 2, 8, 0)
-  GCG_TN_CASE(1, 3, 8, 0)
-  GCG_TN_CASE(1, 3, 12, 0)
-  GCG_TN_CASE(1, 3, 6, 0)
-  GCG_TN_CASE_OCC(1, 3, 2, 0, 2)
-  GCG_TN_CASE_OCC(1, 3, 3, 0, 2)
-  GCG_TN_CASE_OCC(1, 2, 8, 0, 2)
-  GCG_TN_CASE_OCC(1, 2, 4, 0, 2)
-  GCG_TN_CASE_OCC(1, 2, 6, 0, 2)
-  { return fail(GCG_ERR_INVALID_ARG, "%s: no TN tile MG=%d NG=%d PD=%d", fn, p.mg, p.ng, p.pd); }
-#undef GCG_TN_CASE
-#undef GCG_TN_CASE_OCC
-  GCG_HIP_CHECK(hipGetLastError());
-  const int vec = (ldc % 4 == 0 && aligned(C, 16)) ? 1 : 0;
-  const dim3 rgrid(static_cast<unsigned>(((N + 3) / 4 + 63) / 64),
-                   static_cast<unsigned>(std::min<int64_t>(M, 65535)));
-  hipLaunchKernelGGL(gemm_tn_reduce_kernel, rgrid, dim3(64 * kTnRedWaves), 0, s, int(M), int(N),
-                     p.S, part, p.Mp, p.Np, scale_dev, C, ldc, vec);
-  GCG_HIP_CHECK(hipGetLastError());
-  return GCG_OK;
+  return gemm_tn_impl("gcg_gemm_tn_f32", R, M, N, A, lda, B, ldb, scale_dev, C, ldc,
+                      GCG_MATH_F32, 0, workspace, workspace_bytes, stream);
 }
 
 }  // extern "C"

@@ -583,7 +583,7 @@ template <typename TA, typename TACC>
 gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr, const int32_t* a_idx,
                        const TA* a_val, const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
                        int64_t n_products, const int64_t* rowoff_dev, const std::vector<int64_t>& rowoff,
-                       int32_t* c_ptr, int32_t* c_idx, float* c_val, int64_t* nnz_c_dev, hipStream_t st) {
+                       int32_t* c_ptr, int32_t* c_idx, float* c_val, int64_t* nnz_c_dev, hipStream_t st, int flags) {
   (void)nnz_a; (void)n_products;
   constexpr int SMAX = RowsSlab<TACC>::kMax;
   const int64_t n_slabs = (p + SMAX - 1) / SMAX;
@@ -618,7 +618,7 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   auto* id2 = static_cast<int32_t*>(b_id2.p);
   auto* kept = static_cast<int64_t*>(b_kept.p);
   auto* cp64 = static_cast<int64_t*>(b_cp64.p);
-  const int small_ok = (p <= kSmallMaxCols && env_int("GCG_SPGEMM_NO_SMALL") == 0) ? 1 : 0;
+  const int small_ok = (p <= kSmallMaxCols && !(flags & GCG_SPGEMM_DENSE_SLABS)) ? 1 : 0;
   hipLaunchKernelGGL(row_products_u32_kernel, dim3(grid_for(m)), dim3(256), 0, st, m, rowoff_dev, a_ptr, small_ok,
                      key, id);
   GCG_HIP_CHECK(hipGetLastError());
@@ -636,13 +636,12 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   // Measured (tools/exp_spgemm_knobs.py, Twitter-World): the small-row kernel on a side stream
   // beside the dense-slab kernel ran 5x SLOWER (615 vs 112 ms; the two kernels' workgroups
   // compete for LDS), and a persistent grid was no faster than one workgroup per row -- so one
-  // stream, one workgroup per row (GCG_SPGEMM_SMALL_GRID caps the grid for experiments).
-  const int small_grid = env_int("GCG_SPGEMM_SMALL_GRID");
+  // stream, one workgroup per row.
   int col_bits = 1;  // (1 << col_bits) > p: the pad key's column bits exceed every column
   while ((int64_t{1} << col_bits) <= p) ++col_bits;
   auto small_launch = [&](auto kern, int64_t r0, int64_t r1) {
     if (r1 <= r0) return;
-    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(small_grid > 0 ? std::min<int64_t>(r1 - r0, small_grid) : r1 - r0)),
+    hipLaunchKernelGGL(kern, dim3(static_cast<unsigned>(r1 - r0)),
                        dim3(kSmallNT), 0, st, id2 + r0, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, rowoff_dev, tidx,
                        tval, kept, r1 - r0, col_bits);
   };
@@ -664,7 +663,7 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
   if (nnz_c > INT32_MAX) return fail(GCG_ERR_INVALID_ARG, "nnz(C) = %lld exceeds int32 CSR", (long long)nnz_c);
   hipLaunchKernelGGL(cptr32_kernel, dim3(grid_for(m + 1)), dim3(256), 0, st, m, cp64, c_ptr);
   const auto ranges = inplace_ranges(rowoff, cptr);
-  if (ranges.size() <= kMaxInplaceLaunches && env_int("GCG_SPGEMM_COMPACT_TMP") == 0) {
+  if (ranges.size() <= kMaxInplaceLaunches && !(flags & GCG_SPGEMM_COMPACT_TEMPORARY)) {
     for (const auto& rg : ranges)
       hipLaunchKernelGGL(spgemm_compact_inplace_kernel, dim3(grid_for((rg.second - rg.first) * 64)), dim3(256), 0,
                          st, rg.first, rg.second, rowoff_dev, cp64, c_idx, c_val);
@@ -688,20 +687,15 @@ gcg_status spgemm_rows(int64_t m, int64_t p, int64_t nnz_a, const int32_t* a_ptr
 // Products per row chunk: the expand-sort-reduce temporaries are ~40 B per product, so a
 // chunk of 2^29 products holds ~21 GB of HBM; row chunks also keep every hipcub item count
 // and the int32 permutation within range. Twitter-World H.X (2.65e9 products) -> 5 chunks.
-// GCG_SPGEMM_CHUNK (products, > 0) overrides it -- the tests use it to force many chunks.
-int64_t chunk_products() {
-  if (const char* v = std::getenv("GCG_SPGEMM_CHUNK")) {
-    const long long c = std::atoll(v);
-    if (c > 0) return c;
-  }
-  return int64_t{1} << 29;
-}
+// gcg_spgemm_ex's chunk_products (> 0) overrides it -- the tests force many chunks.
+constexpr int64_t kChunkProductsDefault = int64_t{1} << 29;
 
 template <typename TA, typename TACC>
 gcg_status spgemm_impl(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int32_t* a_ptr,
                        const int32_t* a_idx, const TA* a_val, int64_t nnz_b, const int32_t* b_ptr,
                        const int32_t* b_idx, const float* b_val, int64_t n_products, int32_t* c_ptr,
-                       int32_t* c_idx, float* c_val, int64_t* nnz_c_dev, hipStream_t st) {
+                       int32_t* c_idx, float* c_val, int64_t* nnz_c_dev, hipStream_t st, int path,
+                       int64_t chunk_products) {
   (void)n; (void)nnz_b;
   GCG_HIP_CHECK(hipMemsetAsync(nnz_c_dev, 0, sizeof(int64_t), st));
   if (n_products == 0 || nnz_a == 0) {
@@ -743,10 +737,10 @@ gcg_status spgemm_impl(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int
     return fail(GCG_ERR_INVALID_ARG, "n_products %lld != %lld (from gcg_spgemm_products)",
                 (long long)n_products, (long long)rowoff[m]);
   if (m <= INT32_MAX && (p + RowsSlab<TACC>::kMax - 1) / RowsSlab<TACC>::kMax <= kRowsMaxSlabs &&
-      env_int("GCG_SPGEMM_ESC") == 0)
+      !(path & GCG_SPGEMM_EXPAND_SORT))
     return spgemm_rows<TA, TACC>(m, p, nnz_a, a_ptr, a_idx, a_val, b_ptr, b_idx, b_val, n_products, rowoff_dev,
-                                 rowoff, c_ptr, c_idx, c_val, nnz_c_dev, st);
-  const int64_t kChunkProducts = chunk_products();
+                                 rowoff, c_ptr, c_idx, c_val, nnz_c_dev, st, path);
+  const int64_t kChunkProducts = chunk_products > 0 ? chunk_products : kChunkProductsDefault;
   std::vector<int64_t> cuts{0};  // greedy row chunks of <= kChunkProducts products (>= 1 row)
   while (cuts.back() < m) {
     const int64_t r0 = cuts.back();
@@ -906,6 +900,16 @@ gcg_status gcg_spgemm(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int3
                       const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
                       int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
                       float* c_val, int64_t* nnz_c_dev, gcg_stream_t stream) {
+  return gcg_spgemm_ex(m, n, p, nnz_a, a_ptr, a_idx, a_val, a_is_f64, nnz_b, b_ptr, b_idx, b_val,
+                       accumulate_f64, n_products, c_ptr, c_idx, c_val, nnz_c_dev, 0, 0, stream);
+}
+
+gcg_status gcg_spgemm_ex(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int32_t* a_ptr,
+                         const int32_t* a_idx, const void* a_val, int a_is_f64, int64_t nnz_b,
+                         const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
+                         int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
+                         float* c_val, int64_t* nnz_c_dev, int32_t flags, int64_t chunk_products,
+                         gcg_stream_t stream) {
   if (m < 0 || n < 0 || p < 0 || nnz_a < 0 || nnz_b < 0 || n_products < 0 || c_ptr == nullptr ||
       nnz_c_dev == nullptr || a_ptr == nullptr || b_ptr == nullptr)
     return fail(GCG_ERR_INVALID_ARG, "bad args to gcg_spgemm");
@@ -913,15 +917,21 @@ gcg_status gcg_spgemm(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int3
                          b_idx == nullptr || b_val == nullptr))
     return fail(GCG_ERR_INVALID_ARG, "NULL buffer");
   if (a_is_f64 && !accumulate_f64) return fail(GCG_ERR_INVALID_ARG, "float64 A needs accumulate_f64");
+  if (flags & ~(GCG_SPGEMM_EXPAND_SORT | GCG_SPGEMM_DENSE_SLABS | GCG_SPGEMM_COMPACT_TEMPORARY))
+    return fail(GCG_ERR_INVALID_ARG, "unknown gcg_spgemm_ex flags 0x%x", flags);
+  if (chunk_products < 0) return fail(GCG_ERR_INVALID_ARG, "chunk_products < 0");
   hipStream_t st = static_cast<hipStream_t>(stream);
   if (a_is_f64)
     return spgemm_impl<double, double>(m, n, p, nnz_a, a_ptr, a_idx, static_cast<const double*>(a_val), nnz_b,
-                                       b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st);
+                                       b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st,
+                                       flags, chunk_products);
   if (accumulate_f64)
     return spgemm_impl<float, double>(m, n, p, nnz_a, a_ptr, a_idx, static_cast<const float*>(a_val), nnz_b,
-                                      b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st);
+                                      b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st,
+                                      flags, chunk_products);
   return spgemm_impl<float, float>(m, n, p, nnz_a, a_ptr, a_idx, static_cast<const float*>(a_val), nnz_b,
-                                   b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st);
+                                   b_ptr, b_idx, b_val, n_products, c_ptr, c_idx, c_val, nnz_c_dev, st,
+                                   flags, chunk_products);
 }
 
 }  // extern "C"

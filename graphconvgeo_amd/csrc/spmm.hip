@@ -70,7 +70,7 @@ __device__ __forceinline__ Vec<VEC> load_vec(const float* __restrict__ p) {
   return r;
 }
 
-// Non-temporal load (experiment: cold gathered rows, GCG_SPMM_HC).
+// Non-temporal load: the gather hint's cold columns (HC = 1, gcg_spmm_csr_f32_planned_hint).
 template <int VEC>
 __device__ __forceinline__ Vec<VEC> load_vec_nt(const float* __restrict__ p) {
   Vec<VEC> r;
@@ -83,22 +83,6 @@ __device__ __forceinline__ Vec<VEC> load_vec_nt(const float* __restrict__ p) {
     for (int q = 0; q < VEC; ++q) r.x[q] = __builtin_nontemporal_load(p + q);
   }
   return r;
-}
-
-// Non-temporal (streaming) store: Y is written once and not re-read by this kernel, so it
-// need not displace the gathered operand's hot rows from the caches (experiment knob
-// GCG_SPMM_NT_STORE=1).
-template <int VEC>
-__device__ __forceinline__ void store_vec_nt(float* __restrict__ p, const Vec<VEC>& v) {
-  if constexpr (VEC == 4) {
-    typedef float f4v __attribute__((ext_vector_type(4)));
-    __builtin_nontemporal_store(f4v{v.x[0], v.x[1], v.x[2], v.x[3]}, reinterpret_cast<f4v*>(p));
-  } else if constexpr (VEC == 2) {
-    typedef float f2v __attribute__((ext_vector_type(2)));
-    __builtin_nontemporal_store(f2v{v.x[0], v.x[1]}, reinterpret_cast<f2v*>(p));
-  } else {
-    __builtin_nontemporal_store(v.x[0], p);
-  }
 }
 
 template <int VEC>
@@ -153,12 +137,9 @@ __device__ __forceinline__ Vec<VEC> load_bias(const float* __restrict__ b, int c
 
 template <int VEC, int TL>
 __device__ __forceinline__ void store_out(float* __restrict__ yrow, int c, int K,
-                                          const Vec<VEC>& v, int nt) {
+                                          const Vec<VEC>& v) {
   if (!TL || c + VEC <= K) {
-    if (nt)
-      store_vec_nt<VEC>(yrow + c, v);
-    else
-      store_vec<VEC>(yrow + c, v);
+    store_vec<VEC>(yrow + c, v);
     return;
   }
 #pragma unroll
@@ -475,7 +456,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
     if (gate != nullptr) store_gate_t<VEC, TL>(gate + static_cast<int64_t>(p) * ldgate, col[k], K, a);
 #pragma unroll
     for (int q = 0; q < VEC; ++q) a.x[q] = apply_act(a.x[q], act);
-    store_out<VEC, TL>(yrow, col[k], K, a, 0);
+    store_out<VEC, TL>(yrow, col[k], K, a);
   }
 }
 
@@ -492,17 +473,10 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
     const int32_t* __restrict__ out_rows, const float* __restrict__ Z, int64_t ldz, int K,
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
-    float* __restrict__ ws, int64_t ldws, int xcd_remap, uint8_t* __restrict__ gate,
-    int64_t ldgate, int nt_store) {
-  // Optional XCD-aware mapping (experiment): blocks b and b + 8 share an XCD under the
-  // observed round-robin dispatch, so block b takes task block (b % 8) * ceil(nb / 8) + b / 8
-  // and each XCD walks one contiguous range of rows. Placement is speed-only, never correctness.
-  int blk = static_cast<int>(blockIdx.x);
-  if (xcd_remap) {
-    const int nb = static_cast<int>(gridDim.x), per = (nb + 7) / 8;
-    const int cand = (blk % 8) * per + blk / 8;
-    blk = (nb % 8 == 0) ? cand : blk;  // bijective only when 8 divides the grid
-  }
+    float* __restrict__ ws, int64_t ldws, uint8_t* __restrict__ gate, int64_t ldgate) {
+  // (An XCD-aware block -> task mapping was measured and not kept: a random gather has no
+  // per-XCD locality, and it breaks the longest-first task order)
+  const int blk = static_cast<int>(blockIdx.x);
   const int lane = threadIdx.x & (kWave - 1);
   const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
 
@@ -580,7 +554,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
       if (gate != nullptr) store_gate_t<4, TL>(gate + static_cast<int64_t>(p) * ldgate, scol, K, acc);
 #pragma unroll
       for (int q = 0; q < 4; ++q) acc.x[q] = apply_act(acc.x[q], act);
-      store_out<4, TL>(Y + static_cast<int64_t>(p) * ldy, scol, K, acc, nt_store);
+      store_out<4, TL>(Y + static_cast<int64_t>(p) * ldy, scol, K, acc);
     }
     return;
   }
@@ -620,7 +594,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
         store_gate_t<VEC, TL>(gate + static_cast<int64_t>(p) * ldgate, col[k], K, acc[k]);
 #pragma unroll
       for (int q = 0; q < VEC; ++q) acc[k].x[q] = apply_act(acc[k].x[q], act);
-      store_out<VEC, TL>(yrow, col[k], K, acc[k], nt_store);
+      store_out<VEC, TL>(yrow, col[k], K, acc[k]);
     }
   }
 }
@@ -683,21 +657,19 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   // plan-less: one wave per SUB consecutive rows
   const int n_tasks = a.tasks == nullptr ? (a.n_tasks + SUB - 1) / SUB : a.n_tasks;
   const dim3 grid(a.n_coop + (n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
-  static const int xcd = env_int("GCG_XCD_REMAP");
-  const int nts = env_int("GCG_SPMM_NT_STORE");
   if constexpr (VEC == 4) {
     if (a.tail) {
       hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 1>), grid, dim3(kWave * WPB),
                          0, stream, a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices,
                          a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws,
-                         a.ldws, xcd, a.gate, a.ldgate, nts);
+                         a.ldws, a.gate, a.ldgate);
       return;
     }
   }
   hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC>), grid, dim3(kWave * WPB), 0, stream,
                      a.tasks, n_tasks, a.n_coop, a.n_tasks, a.indptr, a.indices, a.vals, a.out_rows,
-                     a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, xcd, a.gate,
-                     a.ldgate, nts);
+                     a.Z, a.ldz, a.K, a.Y, a.ldy, a.bias, a.act, a.ws, a.ldws, a.gate,
+                     a.ldgate);
 }
 
 // Gathers in flight per lane: INFLIGHT floats of Z per lane per batch (U = INFLIGHT/(VEC*NCH)
@@ -706,7 +678,7 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
 // power-law 6.67 vs 6.97 ms, Twitter-US 1.70 vs 1.81 ms, uniform equal; but slower on the
 // small GEOTEXT graph (32-nnz tasks: 39 vs 26 us) and for the narrower variants (K = 64, 128,
 // 129). 256 floats (U = 32) drops to 1 wave/SIMD and halves throughput. So the deep batch is
-// used for the VEC 4 x 2 variant with >= 256-nnz tasks only; GCG_INFLIGHT=64 forces the shallow.
+// used for the VEC 4 x 2 variant with >= 256-nnz tasks only.
 template <int VEC, int NCH, int INFLIGHT>
 void launch_rows_f(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   constexpr int U0 = INFLIGHT / (VEC * NCH);
@@ -722,36 +694,29 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
     // on hub-free graphs -- and loses on a planned power-law task (ordered, World: K = 96 2.08
     // -> 2.54 ms) and at K = 128 (3.09 -> 3.20); World uniform: K = 16 / 32 / 64 1.93 / 1.94 /
     // 2.19 -> 0.91 / 0.93 / 1.48 ms, K = 96 2.50 -> 2.39 (tools/exp_spmm_narrow.py).
-    // GCG_SPMM_SUB = 1 / 2 / 4 forces the rows per wave (experiments, tests).
-    if (a.hint != nullptr && !env_int("GCG_SPMM_NO_HINT")) {  // gather hint (planned only)
+    if (a.hint != nullptr) {  // gather hint (planned only)
       LaunchArgs h = a;
       h.indices = a.hint;
       return launch_rows_u<4, 1, 16, kWavesPerBlock, 1, 1>(h, n_panels, stream);
     }
-    const int sub_env = env_int("GCG_SPMM_SUB");
-    const int sub = sub_env ? sub_env
-                            : (a.tasks != nullptr ? 1 : a.K <= 64 ? 4 : a.K <= 96 ? 2 : 1);
-    if (sub == 4 && a.K <= 64) return launch_rows_u<4, 1, 16, kWavesPerBlock, 4>(a, n_panels, stream);
-    if (sub >= 2 && a.K <= 128) return launch_rows_u<4, 1, 16, kWavesPerBlock, 2>(a, n_panels, stream);
+    if (a.tasks == nullptr && a.K <= 64) return launch_rows_u<4, 1, 16, kWavesPerBlock, 4>(a, n_panels, stream);
+    if (a.tasks == nullptr && a.K <= 96) return launch_rows_u<4, 1, 16, kWavesPerBlock, 2>(a, n_panels, stream);
   }
   if constexpr (VEC == 4 && NCH == 2) {
-    static const int u = env_int("GCG_UNROLL"), inflight = env_int("GCG_INFLIGHT");
-    if (u == 16) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
-    if (u == 24) return launch_rows_u<4, 2, 24, kWavesPerBlock>(a, n_panels, stream);
     // planned tasks of >= 256 nnz: U = 16 since the (col, val) stream is software-pipelined
     // (late round 2): 163 VGPRs / 3 waves per SIMD and fewer SGPR spills than U = 24 (222 VGPRs,
     // 2 waves): World power-law 6.60 vs 6.71 ms (three alternating runs each, one box)
     // gather hint: cold columns' rows gathered non-temporally (gcg_spmm_csr_f32_planned_hint)
-    if (a.hint != nullptr && !env_int("GCG_SPMM_NO_HINT")) {
+    if (a.hint != nullptr) {
       LaunchArgs h = a;
       h.indices = a.hint;
       return launch_rows_u<4, 2, 16, kWavesPerBlock, 1, 1>(h, n_panels, stream);
     }
-    if (inflight != 64 && a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
+    if (a.task_nnz >= 256) return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
     // plan-less, one row per wave, on a large graph (sparse.resolve_auto picks it for graphs
     // without hub rows): U = 16, 3 waves/SIMD -- Twitter-World uniform 9.35-9.36 vs 9.41-9.44 ms
     // at U = 8 (two boxes)
-    if (inflight != 64 && a.tasks == nullptr && a.n_tasks >= 65536)
+    if (a.tasks == nullptr && a.n_tasks >= 65536)
       return launch_rows_u<4, 2, 16, kWavesPerBlock>(a, n_panels, stream);
   }
   launch_rows_f<VEC, NCH, 64>(a, n_panels, stream);
@@ -761,10 +726,10 @@ void launch_rows(const LaunchArgs& a, int n_panels, hipStream_t stream) {
 // implies ldz >= round4(K): the last vector's padding columns are inside the row) runs dwordx4
 // with a masked last vector (*tail = 1) instead of dwordx2 / dword gathers. Measured before
 // (profiles/r03/spmm_k_odd.jsonl, World): C = 930 uniform 29.6 ms as dwordx2 vs 26.5 ms for the
-// 932-wide dwordx4 product on the same rows. GCG_SPMM_NO_TAIL = 1 restores the old choice (A/B).
+// 932-wide dwordx4 product on the same rows. (Operands whose row stride is not a multiple of 4
+// floats still gather dwordx2 / dword vectors: the same products, bitwise.)
 int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K,
              const float* bias, const float* ws, int64_t ldws, int* tail) {
-  const int no_tail = env_int("GCG_SPMM_NO_TAIL");  // read per call: tests toggle it
   *tail = 0;
   for (int vec : {4, 2}) {
     const size_t bytes = sizeof(float) * vec;
@@ -772,7 +737,7 @@ int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K
         (bias == nullptr || aligned(bias, bytes)) &&
         (ws == nullptr || (aligned(ws, bytes) && ldws % vec == 0))) {
       if (K % vec == 0) return vec;
-      if (vec == 4 && !no_tail) {
+      if (vec == 4) {
         *tail = 1;
         return 4;
       }
@@ -781,22 +746,11 @@ int pick_vec(const float* Z, int64_t ldz, const float* Y, int64_t ldy, int64_t K
   return 1;
 }
 
-// Returns panel width (floats) and launches.
-int panel_override() {
-  static const int v = [] {
-    const char* e = std::getenv("GCG_PANEL");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
+// Panel width (floats): up to kPanelMax per launch column (grid.y for the rest).
 gcg_status launch_spmm(const LaunchArgs& a, int vec, hipStream_t stream) {
   const int64_t K = a.K;
-  const int req = panel_override();  // experiment knob: panel width in floats
-  if (req > 0)
-    while (vec > 1 && kWave * vec > req) vec /= 2;
   const int per_chunk = kWave * vec;
-  const int nch_max = req > 0 ? std::max(1, std::min(kPanelMax, req) / per_chunk) : kPanelMax / per_chunk;
+  const int nch_max = kPanelMax / per_chunk;
   int nch = static_cast<int>((K + per_chunk - 1) / per_chunk);
   if (nch > nch_max) nch = nch_max;
   if (nch < 1) nch = 1;
@@ -857,21 +811,13 @@ struct HostPlan {
 };
 
 // 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
-// long rows stay single-wave tasks scheduled first. Default 8 x task_nnz (4096 at Twitter-World);
-// GCG_COOP_MIN = -1 disables the cooperative path (experiment knob). Measured (World power-law,
+// long rows stay single-wave tasks scheduled first: 8 x task_nnz (4096 at Twitter-World). Measured (World power-law,
 // K = 300, slowest of P row blocks, tools/exp_block_modes.py): P = 4 2.12 -> 1.70 ms, P = 8
 // 1.59 -> 1.16 ms, P = 1 and 2 unchanged; thresholds 1024 / 2048 / 4096 within noise of each
 // other. One hub row alone is bound by its CU (~19 GB/s per CU for 1216-B random rows: 0.77 ms
 // for 12,189 nonzeros on 4 waves vs 0.83 on one), so the gain is that hub rows now get a CU
 // each instead of sharing one four to a workgroup.
-int64_t coop_min_nnz(int64_t task_nnz) {
-  static const int v = [] {
-    const char* e = std::getenv("GCG_COOP_MIN");
-    return e ? std::atoi(e) : 0;
-  }();
-  if (v < 0) return INT64_MAX;
-  return v > 0 ? v : 8 * task_nnz;
-}
+int64_t coop_min_nnz(int64_t task_nnz) { return 8 * task_nnz; }
 
 // Default task size: 512 nonzeros, smaller on small graphs so the launch still has
 // >= ~8k waves (256 CUs x 32 waves) to spread; never below 32.

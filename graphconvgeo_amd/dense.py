@@ -8,7 +8,7 @@ Reference (Theano, host BLAS / CPU):
     predict_proba                          softmax rows                       mlpconv.py:329-335
 
 Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
-  matmul(A, W)                    C = A . W          gcg_gemm_nt_f32 on W^T (grad A: g . W^T,
+  matmul(A, W)                    C = A . W          gcg_gemm_nt on W^T (grad A: g . W^T,
                                   the same kernel on W); grad W on gemm_tn
   gemm(A, B) / gemm_nt(A, Bt)     the plain products (register-B / LDS-DMA kernels)
   project_softmax_xent(P, W, b, y)  loss, acc of softmax(P . W + b) against y, one fused
@@ -19,10 +19,13 @@ Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
   gemm_tn(A, B)                   C = A^T . B, the weight gradient h^T . g: a split-K MFMA kernel
                                   (reduction over ~10^6 rows), deterministic
 No product of the layer path goes to hipBLASLt / rocBLAS. There is no CPU path: CPU tensors
-raise. Round 4: gemm_nt (NT_MATH) and the fused layer (GCG_FUSED_MATH) run their products on
-the bf16 matrix cores at f32 accuracy -- every f32 operand split into three bf16 planes, the six
+raise. Round 4: gemm_nt (NT_MATH) and the fused layer (FUSED_MATH) run their products on the
+bf16 matrix cores at f32 accuracy -- every f32 operand split into three bf16 planes, the six
 plane products of order <= 2^-16 accumulated in f32 ("bf16x6"; error against float64 at or
-below the f32 MFMA kernels', tests/test_dense_gpu.py); gemm_tn stays on the f32 MFMA.
+below the f32 MFMA kernels', tests/test_dense_gpu.py; a tile whose result is not finite is
+recomputed on the f32 MFMA, so Inf / NaN follow f32 semantics); gemm_tn stays on the f32 MFMA.
+Round 5: the arithmetic and the tile are arguments of every C call (gcg_gemm_nt,
+gcg_project_softmax_xent, gcg_gemm, gcg_gemm_tn: `math`, `tile`), never the environment.
 """
 from __future__ import annotations
 
@@ -34,6 +37,33 @@ import torch
 
 from . import ops as _ops  # registers torch.ops.gcg.* (the compiled path)
 from ._native import GCG_ACT_NONE, GCG_ACT_RELU, call, load
+
+MATHS = {"f32": 0, "bf16x6": 1}  # gcg_spmm.h GCG_MATH_F32 / GCG_MATH_BF16X6
+
+
+def _math_code(math: str) -> int:
+    if math not in MATHS:
+        raise ValueError(f"math must be one of {tuple(MATHS)}")
+    return MATHS[math]
+
+
+def tile_count(op: str, math: str = "f32") -> int:
+    """Alternative tiles (indices 1..n) of product op ("gemm", "gemm_nt", "fused", "gemm_tn")
+    in arithmetic `math` (gcg_dense_tile_count; -1 when the arithmetic does not exist there)."""
+    ops = {"gemm": 0, "gemm_nt": 1, "fused": 2, "gemm_tn": 3}
+    return int(load().gcg_dense_tile_count(ops[op], _math_code(math)))
+
+
+_WS_SIZES: dict = {}
+
+
+def _ws_bytes(fn: str, N: int, K: int, math: int) -> int:
+    """Workspace bytes of a bf16x6 entry (cached per shape: a host call per step otherwise)."""
+    key = (fn, N, K, math)
+    nb = _WS_SIZES.get(key)
+    if nb is None:
+        nb = _WS_SIZES[key] = int(getattr(load(), fn)(N, K, math))
+    return nb
 from .sparse import _ptr, _require_cuda, _stream_handle, column_sum, empty_dense
 
 FUSED_MAX_COLS = 1024
@@ -90,9 +120,11 @@ class _WeightCache:
 
 
 def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
-         act: Optional[str] = None, out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = act(A . B + bias) on the MFMA kernel. B must have ld >= round4(N) (see
-    _WeightCache); A is copied to an aligned buffer if its rows are not 16-B aligned."""
+         act: Optional[str] = None, out: Optional[torch.Tensor] = None,
+         tile: int = 0) -> torch.Tensor:
+    """C = act(A . B + bias) on the MFMA kernel (gcg_gemm, f32; tile 0: B through LDS, 1: B
+    straight to registers -- bitwise equal). B must have ld >= round4(N) (see _WeightCache); A
+    is copied to an aligned buffer if its rows are not 16-B aligned."""
     A = _aligned_operand(A, "A")
     _require_cuda(B, "B")
     M, K = A.shape
@@ -117,8 +149,8 @@ def gemm(A: torch.Tensor, B: torch.Tensor, bias: Optional[torch.Tensor] = None,
         return out
     actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
     with torch.cuda.device(A.device):
-        call("gcg_gemm_f32", M, N, K, _ptr(A), _ld(A), _ptr(B), ldb, _ptr(bias), actc,
-             _ptr(out), _ld(out), _stream_handle(A.device))
+        call("gcg_gemm", M, N, K, _ptr(A), _ld(A), _ptr(B), ldb, _ptr(bias), actc,
+             _ptr(out), _ld(out), MATHS["f32"], int(tile), _stream_handle(A.device))
     return out
 
 
@@ -132,13 +164,14 @@ NT_MATHS = ("f32", "bf16x6", "bf16x6_inloop")
 
 def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = None,
             act: Optional[str] = None, out: Optional[torch.Tensor] = None,
-            math: Optional[str] = None) -> torch.Tensor:
-    """C = act(A . Bt^T + bias) on the LDS-DMA MFMA kernel (gcg_gemm_nt_f32): both operands
+            math: Optional[str] = None, tile: int = 0) -> torch.Tensor:
+    """C = act(A . Bt^T + bias) on the MFMA NT kernels (gcg_gemm_nt): both operands
     k-contiguous, 16-B aligned rows (A: M x K, Bt: N x K). The weight side is a transposed
     padded copy (_WeightCache(transpose=True)) for A . W, or W itself (padded) for g . W^T.
     math: "f32" (v_mfma_f32_16x16x4_f32) or "bf16x6" (gcg_gemm_nt_f32_bf16x6: f32-accurate
     products from three bf16 planes per operand on the bf16 matrix cores, Bt's planes split
-    once into a workspace; "bf16x6_inloop" splits both operands in the loop); None: NT_MATH."""
+    once into a workspace; "bf16x6_inloop" splits both operands in the loop); None: NT_MATH.
+    tile: 0 = the default for the shape, 1..tile_count("gemm_nt", math) a measured alternative."""
     math = math or NT_MATH
     if math not in NT_MATHS:
         raise ValueError(f"math must be one of {NT_MATHS}")
@@ -163,17 +196,14 @@ def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = No
     if M == 0:
         return out
     actc = {None: GCG_ACT_NONE, "relu": GCG_ACT_RELU, "rectify": GCG_ACT_RELU}[act]
+    code = MATHS["f32" if math == "f32" else "bf16x6"]
+    ws, nb = None, 0
+    if math == "bf16x6":  # Bt's planes split once per call into a workspace (stream-ordered)
+        nb = _ws_bytes("gcg_gemm_nt_workspace", N, K, code)
+        ws = torch.empty(nb, dtype=torch.uint8, device=A.device)
     with torch.cuda.device(A.device):
-        if math == "f32":
-            call("gcg_gemm_nt_f32", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt), _ptr(bias), actc,
-                 _ptr(out), _ld(out), _stream_handle(A.device))
-        else:
-            ws, nb = None, 0
-            if math == "bf16x6":
-                nb = int(load().gcg_gemm_nt_bf16x6_workspace(N, K))
-                ws = torch.empty(nb, dtype=torch.uint8, device=A.device)  # stream-ordered
-            call("gcg_gemm_nt_f32_bf16x6", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt),
-                 _ptr(bias), actc, _ptr(out), _ld(out), _ptr(ws), nb, _stream_handle(A.device))
+        call("gcg_gemm_nt", M, N, K, _ptr(A), _ld(A), _ptr(Bt), _ld(Bt), _ptr(bias), actc,
+             _ptr(out), _ld(out), code, int(tile), _ptr(ws), nb, _stream_handle(A.device))
     return out
 
 
@@ -181,9 +211,10 @@ _TN_WS: dict = {}
 
 
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = None,
-            out: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """C = scale * A^T . B (the weight gradient h^T . g) on the split-K MFMA kernel;
-    deterministic (partials summed in a fixed order). scale: optional device scalar."""
+            out: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
+    """C = scale * A^T . B (the weight gradient h^T . g) on the split-K MFMA kernel (gcg_gemm_tn,
+    f32); deterministic (partials summed in a fixed order). scale: optional device scalar.
+    tile: 0 = the default layout for the shape, 1..tile_count("gemm_tn") another one."""
     A = _aligned_operand(A, "A")
     B = _aligned_operand(B, "B")
     R, M = A.shape
@@ -203,7 +234,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
     if R == 0:
         return out.zero_()
     nb = C.c_size_t()
-    call("gcg_gemm_tn_f32_workspace_bytes", R, M, N, C.byref(nb))
+    call("gcg_gemm_tn_workspace_bytes", R, M, N, MATHS["f32"], int(tile), C.byref(nb))
     key = (A.device, torch.cuda.current_stream(A.device).cuda_stream)
     ws = _TN_WS.get(key)
     if ws is None or ws.numel() * 4 < nb.value:
@@ -212,9 +243,9 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
     if scale is not None:
         scale = scale.reshape(1).to(torch.float32).contiguous()
     with torch.cuda.device(A.device):
-        call("gcg_gemm_tn_f32", R, M, N, _ptr(A), _ld(A), _ptr(B), _ld(B), _ptr(scale),
-             _ptr(out), out.stride(0) if M > 1 else N, _ptr(ws), ws.numel() * 4,
-             _stream_handle(A.device))
+        call("gcg_gemm_tn", R, M, N, _ptr(A), _ld(A), _ptr(B), _ld(B), _ptr(scale),
+             _ptr(out), out.stride(0) if M > 1 else N, MATHS["f32"], int(tile), _ptr(ws),
+             ws.numel() * 4, _stream_handle(A.device))
     return out
 
 
@@ -416,14 +447,21 @@ def _row_weight(w: Optional[torch.Tensor], M: int) -> Optional[torch.Tensor]:
     return w.detach().to(torch.float32).contiguous()
 
 
-# fused layer (bf16x6): W's planes pre-split once per call into a workspace laid out for
-# coalesced loads (FX = 1) instead of split in every workgroup's registers; at N > 768 on a
-# 64-row tile -- World 840k x 300 x 930 140-147.5 vs 121-128 TFLOP/s f32-equivalent
-# (tools/exp_fused_compose.py, test_fused6_row_bands_bitwise)
+# The fused layer's default arithmetic (gcg_project_softmax_xent `math`): "bf16x6" (f32-accurate
+# products on the bf16 matrix cores) or "f32" (v_mfma_f32_16x16x4_f32).
+FUSED_MATH = "bf16x6"
+# bf16x6: W's planes pre-split once per call into a workspace laid out for coalesced loads
+# (FX = 1) instead of split in every workgroup's registers; at N > 768 on a 64-row tile -- World
+# 840k x 300 x 930 140-147.5 vs 121-128 TFLOP/s f32-equivalent (tools/exp_fused_compose.py,
+# test_fused6_row_bands_bitwise)
 FUSED_PRESPLIT = True
 
 
-def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weight=None):
+def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weight=None,
+           math: Optional[str] = None, tile: int = 0):
+    """gcg_project_softmax_xent with an explicit arithmetic (None: FUSED_MATH) and tile."""
+    math = math or FUSED_MATH
+    code = _math_code(math)
     P = _aligned_operand(P, "P")
     M, K = P.shape
     N = Wp.shape[1]
@@ -437,14 +475,14 @@ def _fused(P, Wp, b, labels, scale, scale_dev, out, loss_rows, correct, row_weig
     if M == 0:
         return
     ws, nb = None, 0
-    if FUSED_PRESPLIT:  # the weight's bf16 planes split once per call into a workspace
-        nb = int(load().gcg_project_softmax_xent_bf16x6_workspace(N, K))
+    if math == "bf16x6" and FUSED_PRESPLIT:  # the weight's bf16 planes, split once per call
+        nb = _ws_bytes("gcg_project_softmax_xent_workspace", N, K, code)
         ws = torch.empty(nb, dtype=torch.uint8, device=P.device)
     with torch.cuda.device(P.device):
-        call("gcg_project_softmax_xent_weighted_ws_f32", M, N, K, _ptr(P), _ld(P), _ptr(Wp),
-             Wp.stride(0), _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
+        call("gcg_project_softmax_xent", M, N, K, _ptr(P), _ld(P), _ptr(Wp), Wp.stride(0),
+             _ptr(b), _ptr(labels), float(scale), _ptr(scale_dev), _ptr(out),
              _ld(out) if out is not None else 0, _ptr(loss_rows), _ptr(correct),
-             _ptr(row_weight), _ptr(ws), nb, _stream_handle(P.device))
+             _ptr(row_weight), code, int(tile), _ptr(ws), nb, _stream_handle(P.device))
 
 
 class _ProjectXent(torch.autograd.Function):

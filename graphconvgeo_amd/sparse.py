@@ -482,12 +482,11 @@ def _check_dense(Z: torch.Tensor, A: DeviceCSR):
 def _gathers_vec4(Z, ldz: int, Y, ldy: int, K: int, bias) -> bool:
     """Whether the SpMM launch gathers 16-B vectors (spmm.hip pick_vec): ldz, ldy multiples of
     4 floats, 16-B aligned Z / Y / bias. Since round 4 any K (a masked last vector when
-    K % 4 != 0, unless GCG_SPMM_NO_TAIL=1)."""
+    K % 4 != 0). The layout alone decides it (round 5: no environment knob -- ADVICE r04)."""
+    del K
     if ldz % 4 or ldy % 4 or Z.data_ptr() % 16 or Y.data_ptr() % 16:
         return False
-    if bias is not None and bias.data_ptr() % 16:
-        return False
-    return K % 4 == 0 or os.environ.get("GCG_SPMM_NO_TAIL", "0") in ("", "0")
+    return bias is None or bias.data_ptr() % 16 == 0
 
 
 WIDE_ROW_ALIGN = True  # row_stride: 256-B aligned rows above 512 floats (False: round-3 rule, A/B)
@@ -761,13 +760,20 @@ def scatter_add_rows(out: torch.Tensor, seg_ptr: torch.Tensor, sorted_pos: torch
     return out
 
 
+SPGEMM_FLAGS = {"expand_sort": 1, "dense_slabs": 2, "compact_temporary": 4}  # gcg_spgemm_ex
+
+
 def spgemm(A: DeviceCSR, B: DeviceCSR, accumulate_f64: bool = False,
-           a_data64: Optional[torch.Tensor] = None) -> DeviceCSR:
+           a_data64: Optional[torch.Tensor] = None, paths=(), chunk_products: int = 0) -> DeviceCSR:
     """C = A . B on the GPU (the input convolution X_conv = H * X, main.py:530).
 
     a_data64: float64 values of A (the reference's H is float64 there; implies float64
     accumulation). Entries are summed in scipy's csr_matmat order; exact zeros dropped;
-    output canonical float32 (= `(H * X).tocsr().astype('float32')`)."""
+    output canonical float32 (= `(H * X).tocsr().astype('float32')`). paths / chunk_products
+    force a path of gcg_spgemm_ex (names of SPGEMM_FLAGS; tests): every path, the same C."""
+    flags = 0
+    for name in paths:
+        flags |= SPGEMM_FLAGS[name]
     if not isinstance(A, DeviceCSR) or not isinstance(B, DeviceCSR):
         raise ValueError("spgemm operands must be DeviceCSR")
     if A.n_cols != B.n_rows:
@@ -790,9 +796,10 @@ def spgemm(A: DeviceCSR, B: DeviceCSR, accumulate_f64: bool = False,
             a_vals, is64, acc64 = a_data64.contiguous(), 1, 1
         else:
             a_vals, is64, acc64 = A.data, 0, int(bool(accumulate_f64))
-        call("gcg_spgemm", A.n_rows, A.n_cols, B.n_cols, A.nnz, _ptr(A.indptr), _ptr(A.indices),
-             _ptr(a_vals), is64, B.nnz, _ptr(B.indptr), _ptr(B.indices), _ptr(B.data), acc64,
-             P.value, _ptr(c_ptr), _ptr(c_idx), _ptr(c_val), _ptr(nnz), stream)
+        call("gcg_spgemm_ex", A.n_rows, A.n_cols, B.n_cols, A.nnz, _ptr(A.indptr),
+             _ptr(A.indices), _ptr(a_vals), is64, B.nnz, _ptr(B.indptr), _ptr(B.indices),
+             _ptr(B.data), acc64, P.value, _ptr(c_ptr), _ptr(c_idx), _ptr(c_val), _ptr(nnz), flags,
+             int(chunk_products), stream)
     m = int(nnz.item())
     # exact-size copies: the capacity-P buffers (products; 2.5x nnz(C) at Twitter-World) go
     # back to the caching allocator and serve the next call instead of staying pinned by C

@@ -306,6 +306,18 @@ gcg_status gcg_spgemm(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int3
                       const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
                       int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
                       float* c_val, int64_t* nnz_c_dev, gcg_stream_t stream);
+/* gcg_spgemm with the path forced (tests, measurement; every path gives the same C, bitwise):
+ * flags GCG_SPGEMM_EXPAND_SORT = the expand-sort-reduce path at any p, GCG_SPGEMM_DENSE_SLABS =
+ * every row on the dense LDS slabs (no short-row radix-sort kernel), GCG_SPGEMM_COMPACT_TEMPORARY
+ * = compact C through an nnz(C)-sized temporary instead of in place; chunk_products > 0 caps the
+ * products per expand-sort-reduce row chunk (0 = 2^29). gcg_spgemm = flags 0, chunk 0. */
+enum { GCG_SPGEMM_EXPAND_SORT = 1, GCG_SPGEMM_DENSE_SLABS = 2, GCG_SPGEMM_COMPACT_TEMPORARY = 4 };
+gcg_status gcg_spgemm_ex(int64_t m, int64_t n, int64_t p, int64_t nnz_a, const int32_t* a_ptr,
+                         const int32_t* a_idx, const void* a_val, int a_is_f64, int64_t nnz_b,
+                         const int32_t* b_ptr, const int32_t* b_idx, const float* b_val,
+                         int accumulate_f64, int64_t n_products, int32_t* c_ptr, int32_t* c_idx,
+                         float* c_val, int64_t* nnz_c_dev, int32_t flags, int64_t chunk_products,
+                         gcg_stream_t stream);
 
 /*
  * Mention-graph projection on the device (DataLoader.get_graph's celebrity filter,
@@ -325,70 +337,122 @@ gcg_status gcg_project_mention_graph(int64_t n_targets, int64_t n_nodes, int64_t
                                      int64_t* n_edges, int32_t* status_dev, gcg_stream_t stream);
 
 /*
- * Dense side of the output layer on the matrix cores (v_mfma_f32_16x16x4_f32: f32 in, f32
- * accumulate; the k order inside a 16-deep step is permuted, so results equal a BLAS sgemm
- * within f32 rounding, not bit for bit). Row-major operands; A: M x K (lda), B: K x N (ldb),
- * C: M x N (ldc). A and B need 16-B aligned bases and ld % 4 == 0; B is read at columns
- * < round4(N), so ldb >= round4(N) (pad the weight, as graphconvgeo_amd.dense does).
+ * Dense side of the output layer on the matrix cores. Row-major operands; A: M x K (lda),
+ * B: K x N (ldb), C: M x N (ldc). A and B need 16-B aligned bases and ld % 4 == 0; B is read at
+ * columns < round4(N), so ldb >= round4(N) (pad the weight, as graphconvgeo_amd.dense does).
  *
- * gcg_gemm_f32: C = act(A . B + bias)        T.dot(h, W) (+ b) at mlpconv.py:88 / the
- *   propagate-first form of mlpconv.py:88-93, and Theano's g . W^T (W^T passed as B).
+ * Arithmetic and tile are explicit per call (round 5) -- no environment variable changes what a
+ * dense entry computes:
+ *   math  GCG_MATH_F32     v_mfma_f32_16x16x4_f32: exact f32 products, f32 accumulation; the k
+ *                          order inside a 16-deep step is permuted (step s takes k = k0 + 4q + s),
+ *                          so results equal a BLAS sgemm within f32 rounding, not bit for bit.
+ *         GCG_MATH_BF16X6  f32 on the bf16 matrix cores: every f32 operand split into three bf16
+ *                          planes x = x0 + x1 + x2 (round to nearest, 8 significant bits each), the
+ *                          six plane products of order <= 2^-16 accumulated in f32
+ *                          (v_mfma_f32_16x16x32_bf16), each exact. The planes hold x exactly
+ *                          (3 x 8 significant bits), |x1| <= 2^-8 |x|, |x2| <= 2^-17 |x|, so the
+ *                          dropped a1b2 + a2b1 + a2b2 are <= (2^-24 + 2^-34) |a||b| per product --
+ *                          one f32 rounding of the product (tests/test_bf16x6_numerics.py pins
+ *                          these bounds; tests/test_dense_gpu.py the whole product's error against
+ *                          float64, <= 1.25 x the f32 kernel's).
+ *                          f32 semantics at the edges: a tile whose bf16x6 result is not finite
+ *                          (an infinite operand, |x| above bf16's largest finite 3.39e38, NaN, or
+ *                          overflow) is recomputed on the f32 MFMA in the f32 kernel's k order, so
+ *                          +-Inf propagates and Inf * 0 gives NaN exactly as with GCG_MATH_F32.
+ *   tile  0 = the default tile, a pure function of (M, N, K); 1..gcg_dense_tile_count(op, math)
+ *         = a measured alternative (tests, measurement); the same products except where noted.
  */
+enum { GCG_MATH_F32 = 0, GCG_MATH_BF16X6 = 1 };
+enum { GCG_DENSE_GEMM = 0, GCG_DENSE_GEMM_NT = 1, GCG_DENSE_FUSED = 2, GCG_DENSE_GEMM_TN = 3 };
+/* Alternative tiles of product op (GCG_DENSE_*) in arithmetic math: tile indices 1..n are valid;
+ * -1 when that arithmetic is not available for the product. */
+int32_t gcg_dense_tile_count(int32_t op, int32_t math);
+
+/*
+ * gcg_gemm: C = act(A . B + bias)        T.dot(h, W) (+ b) at mlpconv.py:88 / the propagate-first
+ *   form of mlpconv.py:88-93, and Theano's g . W^T (W^T passed as B). GCG_MATH_F32 only; tile 0
+ *   stages B through LDS (gemm_bl_kernel), tile 1 reads it straight into registers (gemm_kernel):
+ *   the same k order, bitwise equal.
+ * gcg_gemm_f32 = gcg_gemm(..., GCG_MATH_F32, 0, ...).
+ */
+gcg_status gcg_gemm(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* B,
+                    int64_t ldb, const float* bias /*nullable*/, int act, float* C, int64_t ldc,
+                    int32_t math, int32_t tile, gcg_stream_t stream);
 gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                         const float* B, int64_t ldb, const float* bias /*nullable*/, int act,
                         float* C, int64_t ldc, gcg_stream_t stream);
 
 /*
- * gcg_gemm_nt_f32: C = act(A . Bt^T + bias) with the second operand stored transposed
- * (Bt: N x K row-major, ldbt >= round4(K), ldbt % 4 == 0, 16-B aligned base; A likewise with
- * lda). The projection T.dot(h, W) (mlpconv.py:88) with Bt = W^T, and Theano's input
- * gradient g . W^T with Bt = W itself. Both operands are k-contiguous, so both go to LDS
- * through the asynchronous LDS-DMA (global_load_lds) into a ring of k chunks (default: 16-deep
- * chunks, 4 stages); in the 16-deep step that reaches past K the fragment elements at k >= K
- * are zeroed in registers, so operand padding may hold anything (NaN included). Same numerics
- * as gcg_gemm_f32.
+ * gcg_gemm_nt: C = act(A . Bt^T + bias) with the second operand stored transposed (Bt: N x K
+ * row-major, ldbt >= round4(K), ldbt % 4 == 0, 16-B aligned base; A likewise with lda). The
+ * projection T.dot(h, W) (mlpconv.py:88) with Bt = W^T, and Theano's input gradient g . W^T with
+ * Bt = W itself. In the k step that reaches past K the fragment elements at k >= K are zeroed in
+ * registers, so operand padding may hold anything (NaN included).
+ *   GCG_MATH_F32: both operands through the asynchronous LDS-DMA (global_load_lds) into a ring of
+ *     k chunks (tile 0: 16-deep chunks, 4 stages); every tile the same k order.
+ *   GCG_MATH_BF16X6: ws != NULL (gcg_gemm_nt_workspace(N, K, math) bytes, 16-B aligned): Bt's
+ *     three planes split once per call into it by a small kernel on the same stream, A split in
+ *     registers (tile 0: A in registers, 128 x 64 G columns with G padding N least); ws == NULL:
+ *     both operands split in the loop (tile 0 only). Every bf16x6 form accumulates the same six
+ *     plane products in the same order: bitwise equal to each other.
+ * gcg_gemm_nt_f32 = gcg_gemm_nt(..., GCG_MATH_F32, 0, NULL, 0, ...);
+ * gcg_gemm_nt_f32_bf16x6 = gcg_gemm_nt(..., GCG_MATH_BF16X6, 0, ws, ws_bytes, ...).
  */
+gcg_status gcg_gemm_nt(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                       const float* Bt, int64_t ldbt, const float* bias /*nullable*/, int act,
+                       float* C, int64_t ldc, int32_t math, int32_t tile, void* ws /*nullable*/,
+                       int64_t ws_bytes, gcg_stream_t stream);
+int64_t gcg_gemm_nt_workspace(int64_t N, int64_t K, int32_t math);
 gcg_status gcg_gemm_nt_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                            const float* Bt, int64_t ldbt, const float* bias /*nullable*/,
                            int act, float* C, int64_t ldc, gcg_stream_t stream);
-
-/*
- * gcg_gemm_nt_f32_bf16x6: gcg_gemm_nt_f32 (same operands, layout rules and padding guarantee)
- * with the products on the bf16 matrix cores: every f32 fragment is split in registers into
- * three bf16 planes x = x0 + x1 + x2 (round to nearest, 8 significant bits each) and the six
- * plane products of order <= 2^-16 are accumulated in f32 (v_mfma_f32_16x16x32_bf16), each
- * exact. Accuracy is f32's: the dropped cross terms are <= 2^-25 |a||b| per product, below the
- * rounding of an f32 accumulation (tests/test_dense_gpu.py compares the error against float64
- * with the f32 kernel's). NaN propagates; an infinite operand yields NaN instead of +-Inf.
- */
 gcg_status gcg_gemm_nt_f32_bf16x6(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
                                   const float* Bt, int64_t ldbt, const float* bias /*nullable*/,
                                   int act, float* C, int64_t ldc, void* ws /*nullable*/,
                                   int64_t ws_bytes, gcg_stream_t stream);
-/* Workspace of gcg_gemm_nt_f32_bf16x6 (bytes, 16-B aligned): Bt's three planes, split once per
- * call by a small kernel on the same stream, so the loop converts only A. ws == NULL splits
- * both operands inside the loop instead (same products, bitwise). */
+/* = gcg_gemm_nt_workspace(N, K, GCG_MATH_BF16X6) */
 int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K);
 
 /*
  * Fused output layer + loss (N <= 1024; one workgroup owns whole rows):
  *   logits = A . W + bias                                       mlpconv.py:88-93
- *   labels != NULL: out = (softmax(logits) - onehot(labels)) * scale   (the logits gradient
- *     of categorical_crossentropy(...).mean() with scale = 1/M, mlpconv.py:229-230),
- *     loss_rows[i] = -log softmax(logits)[i, labels[i]],
- *     correct_rows[i] (nullable) = 1 if the first-index argmax equals labels[i] else 0
+ *   labels != NULL: out = (softmax(logits) - onehot(labels)) * scale * row_weight[i]  (the logits
+ *     gradient of categorical_crossentropy(...).mean() with scale = 1/M, mlpconv.py:229-230),
+ *     loss_rows[i] = -log softmax(logits)[i, labels[i]] * row_weight[i],
+ *     correct_rows[i] (nullable) = row_weight[i] if the first-index argmax equals labels[i] else 0
  *     (argmax + T.eq accuracy, mlpconv.py:227,252);
  *   labels == NULL: out = softmax(logits) (predict_proba, mlpconv.py:329-335);
  *   out may be NULL when labels are given (evaluation: loss and accuracy only).
- * scale_dev (nullable, device): multiplies scale (the upstream gradient of the loss, read
- * on the device so the call can sit inside a captured HIP graph). The logits never reach HBM.
- * out needs ldo % 4 == 0 and a 16-B aligned base; its padding columns [N, round4(N)) are
- * written with zeros (whole dwordx4 row stores). W's padding columns [N, ldw) may hold
- * anything (NaN included): they never reach a logit.
- * Products (round 4): on the bf16 matrix cores at f32 accuracy (three bf16 planes per f32
- * operand, six plane products, as gcg_gemm_nt_f32_bf16x6); the environment variable
- * GCG_FUSED_MATH=f32 selects the f32 MFMA kernel (v_mfma_f32_16x16x4_f32).
+ * row_weight (device, nullable = all 1, then bitwise the unweighted result): with the distinct
+ * targets as rows and their multiplicities as weights, one call computes the loss and gradient of
+ * a target list drawn with replacement (tensormain.py:226) over its distinct rows only.
+ * scale_dev (nullable, device): multiplies scale (the upstream gradient of the loss, read on the
+ * device so the call can sit inside a captured HIP graph). The logits never reach HBM. out needs
+ * ldo % 4 == 0 and a 16-B aligned base; its padding columns [N, round4(N)) are written with zeros
+ * (whole dwordx4 row stores). W's padding columns [N, ldw) may hold anything (NaN included): they
+ * never reach a logit. A label outside [0, N) gives that row a NaN loss, no hit, no onehot.
+ *   GCG_MATH_F32 (gemm_kernel): 32 rows x 4 waves; tiles 1..5 split the weight's register set
+ *     into 0 / 2 / 4 / 8 / 16 rotating parts (tile 0: 8 at N > 768, else 4) -- bitwise equal.
+ *   GCG_MATH_BF16X6 (gemm_fused6_kernel): ws != NULL (gcg_project_softmax_xent_workspace(N, K,
+ *     math) bytes, 16-B aligned): the weight's three bf16 planes split once per call into it;
+ *     tile 0 = 64 rows x 8 waves at N > 768 (row sums over 8 column waves), else 32 rows x 4
+ *     waves; tile 1 = 32 rows x 4 waves at any N (bitwise the ws == NULL form); tile 2 = the
+ *     64-row form (N > 768 only). ws == NULL: the weight split in every workgroup's registers,
+ *     32 rows x 4 waves (tile 0 only). The 64-row form is within f32 rounding of the 32-row one
+ *     (another association of the row sums), with the same hits.
+ * Legacy entries: gcg_project_softmax_xent_f32 and _weighted_f32 = GCG_MATH_F32, tile 0;
+ * _weighted_ws_f32 = GCG_MATH_BF16X6, tile 0 (with ws, or the in-register split when NULL).
  */
+gcg_status gcg_project_softmax_xent(int64_t M, int64_t N, int64_t K, const float* A, int64_t lda,
+                                    const float* W, int64_t ldw, const float* bias /*nullable*/,
+                                    const int32_t* labels /*nullable*/, float scale,
+                                    const float* scale_dev /*nullable*/, float* out /*nullable*/,
+                                    int64_t ldo, float* loss_rows,
+                                    float* correct_rows /*nullable*/,
+                                    const float* row_weight /*nullable*/, int32_t math,
+                                    int32_t tile, void* ws /*nullable*/, int64_t ws_bytes,
+                                    gcg_stream_t stream);
+int64_t gcg_project_softmax_xent_workspace(int64_t N, int64_t K, int32_t math);
 gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const float* A,
                                         int64_t lda, const float* W, int64_t ldw,
                                         const float* bias /*nullable*/,
@@ -396,18 +460,7 @@ gcg_status gcg_project_softmax_xent_f32(int64_t M, int64_t N, int64_t K, const f
                                         const float* scale_dev /*nullable*/,
                                         float* out /*nullable*/, int64_t ldo, float* loss_rows,
                                         float* correct_rows /*nullable*/, gcg_stream_t stream);
-
-/*
- * gcg_project_softmax_xent_weighted_ws_f32: gcg_project_softmax_xent_weighted_f32 with a
- * workspace (bytes: gcg_project_softmax_xent_bf16x6_workspace(N, K), 16-B aligned): on the bf16
- * matrix cores the weight's three bf16 planes are split once per call into it (a small kernel on
- * the same stream) instead of in every workgroup's registers, and at N > 768 on 64-row tiles
- * (8 waves; row sums over 8 column waves: within f32 rounding of the plain entry, the same
- * hits); 10-20 % faster at Twitter-World's shapes; the package's default path
- * (graphconvgeo_amd/dense.py). GCG_FUSED6_FX_NARROW=1: 32-row tiles, bitwise the plain entry.
- * ws == NULL or GCG_FUSED_MATH=f32: the plain entry's kernels; a workspace smaller than
- * gcg_project_softmax_xent_bf16x6_workspace(N, K): GCG_ERR_INVALID_ARG.
- */
+/* = gcg_project_softmax_xent_workspace(N, K, GCG_MATH_BF16X6) */
 int64_t gcg_project_softmax_xent_bf16x6_workspace(int64_t N, int64_t K);
 gcg_status gcg_project_softmax_xent_weighted_ws_f32(
     int64_t M, int64_t N, int64_t K, const float* A, int64_t lda, const float* W, int64_t ldw,
@@ -457,11 +510,21 @@ gcg_status gcg_softmax_xent_weighted_f32(int64_t M, int64_t N, const float* logi
 /*
  * Weight gradient C = scale * A^T . B (Theano's grad of T.dot(h, W) w.r.t. W: h^T . gz,
  * mlpconv.py:88; P^T . G in the propagate-first order), A: R x M, B: R x N, C: M x N, the
- * reduction over R (~10^6 rows) split across workgroups on the f32 MFMA path; the per-split
- * partials (caller-owned workspace, size from _workspace_bytes) are summed in split order, so
- * the result is deterministic (equal to a BLAS sgemm within f32 rounding). A and B: 16-B aligned,
- * lda >= round4(M), ldb >= round4(N), ld % 4 == 0. scale_dev: nullable device scalar.
+ * reduction over R (~10^6 rows) split across waves on the f32 MFMA; the per-split partials
+ * (caller-owned workspace, size from gcg_gemm_tn_workspace_bytes for the same math and tile) are
+ * summed in split order, so the result is deterministic (equal to a BLAS sgemm within f32
+ * rounding). A and B: 16-B aligned, lda >= round4(M), ldb >= round4(N), ld % 4 == 0. scale_dev:
+ * nullable device scalar. GCG_MATH_F32 only; tile 0 = per-wave 64 x 64 NG tiles (NG padding N
+ * least) or, for M <= 256 in 64-row bands with N <= 512, waves stacked along M; tiles 1..7 =
+ * other wave layouts and split counts (another summation order: within f32 rounding).
+ * gcg_gemm_tn_f32[_workspace_bytes] = the GCG_MATH_F32, tile 0 forms.
  */
+gcg_status gcg_gemm_tn_workspace_bytes(int64_t R, int64_t M, int64_t N, int32_t math,
+                                       int32_t tile, size_t* bytes);
+gcg_status gcg_gemm_tn(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
+                       const float* B, int64_t ldb, const float* scale_dev /*nullable*/, float* C,
+                       int64_t ldc, int32_t math, int32_t tile, void* workspace,
+                       size_t workspace_bytes, gcg_stream_t stream);
 gcg_status gcg_gemm_tn_f32_workspace_bytes(int64_t R, int64_t M, int64_t N, size_t* bytes);
 gcg_status gcg_gemm_tn_f32(int64_t R, int64_t M, int64_t N, const float* A, int64_t lda,
                            const float* B, int64_t ldb, const float* scale_dev /*nullable*/,

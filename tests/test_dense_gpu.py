@@ -93,8 +93,8 @@ def test_gemm_rejects_bad_operands(cuda):
 @pytest.mark.parametrize("math", ["bf16x6", "f32"])
 def test_fused_softmax_xent_vs_float64(cuda, M, K, N, math, monkeypatch):
     """The fused output layer, on the bf16 matrix cores (gemm_fused6_kernel, the default) and on
-    the f32 MFMA (GCG_FUSED_MATH=f32, gemm_kernel): loss, gradient, hits, probabilities."""
-    monkeypatch.setenv("GCG_FUSED_MATH", math)
+    the f32 MFMA (math GCG_MATH_F32, gemm_kernel): loss, gradient, hits, probabilities."""
+    monkeypatch.setattr(dense, "FUSED_MATH", math)
     P, W, b = _rand((M, K), 11, 0.3), _rand((K, N), 12, 0.3), _rand((N,), 13)
     y = np.random.default_rng(14).integers(0, N, M).astype(np.int32)
     proj = dense.Projection()
@@ -126,7 +126,7 @@ def test_fused_labels_outside_classes(cuda, N, math, monkeypatch):
     """A label outside [0, N) (-1, N, N + 7; the C-ABI does not check labels on the host): that
     row's loss is NaN, its hit 0, and its gradient row the probabilities times scale (no onehot
     subtracted); every other row as with valid labels. Both maths, the 64-row tile at N = 930."""
-    monkeypatch.setenv("GCG_FUSED_MATH", math)
+    monkeypatch.setattr(dense, "FUSED_MATH", math)
     M, K = 70, 33
     P, W, b = _rand((M, K), 61, 0.3), _rand((K, N), 62, 0.3), _rand((N,), 63)
     y = np.random.default_rng(64).integers(0, N, M).astype(np.int32)
@@ -157,7 +157,7 @@ def test_fused_labels_outside_classes(cuda, N, math, monkeypatch):
 def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N, math, monkeypatch):
     """W's padding columns [N, ldw) may hold anything (gcg_spmm.h): NaN there must not reach
     the softmax sum, the loss or the gradient -- bitwise the zero-padded result."""
-    monkeypatch.setenv("GCG_FUSED_MATH", math)
+    monkeypatch.setattr(dense, "FUSED_MATH", math)
     P, W, b = _rand((M, K), 31, 0.3), _rand((K, N), 32, 0.3), _rand((N,), 33)
     y = np.random.default_rng(34).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
@@ -181,22 +181,21 @@ def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N, math, monkeypatch):
 
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (300, 300, 256), (513, 300, 930), (70, 33, 1024),
                                    (40, 50, 300), (33, 70, 700), (65, 17, 900)])
-def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
-    """The B ping-pong split (GCG_GEMM_SPLIT = 0 / 2 / 4 / 8 / 16 register-set parts) only reorders
-    MFMAs between distinct accumulators: gradient, loss and hits are bitwise equal (the f32 MFMA
-    kernel, GCG_FUSED_MATH=f32)."""
-    monkeypatch.setenv("GCG_FUSED_MATH", "f32")
+def test_fused_split_pingpong_bitwise(cuda, M, K, N):
+    """The f32 MFMA fused layer's tiles 1..5 (the B register set split into 0 / 2 / 4 / 8 / 16
+    rotating parts) only reorder MFMAs between distinct accumulators: gradient, loss and hits
+    bitwise equal to tile 0 (the default)."""
+    assert dense.tile_count("fused", "f32") == 5
     P, W, b = _rand((M, K), 21, 0.3), _rand((K, N), 22, 0.3), _rand((N,), 23)
     y = np.random.default_rng(24).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
     yt = torch.from_numpy(y).to(cuda)
     Wp = dense.Projection().fwd.get(Wt, False)
     outs = []
-    for split in ("0", "2", "4", "8", "16"):
-        monkeypatch.setenv("GCG_GEMM_SPLIT", split)
+    for tile in range(6):
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
-        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
+        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits, math="f32", tile=tile)
         outs.append((G, loss, hits))
     for G, loss, hits in outs[1:]:
         assert torch.equal(G, outs[0][0]) and torch.equal(loss, outs[0][1])
@@ -206,39 +205,40 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N, monkeypatch):
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
                                    (9, 4, 61), (5, 7, 801), (128, 64, 1021)])
 def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
-    """gemm_fused6_kernel's forms: the weight split in registers (dense.FUSED_PRESPLIT off) with
-    one row band (4 waves), two row bands (GCG_FUSED6_WR=2, 8 waves) and the wide 64-row tile
-    (GCG_FUSED6_WIDE=1: 8 waves x 128 columns, one W register set, N > 768); the weight's planes
-    pre-split into a workspace (the default) with the wide tile (the default at N > 768) and the
-    4-wave tile (GCG_FUSED6_FX_NARROW=1). The same products in the same order per element: the 4-wave forms
-    and the two-band form are bitwise equal (gradient, loss, hits, probabilities), rows past M
-    included; the wide tiles' row sums run over 8 column waves (another association): within
-    f32 rounding, the same hits."""
-    monkeypatch.setenv("GCG_FUSED_MATH", "bf16x6")
+    """gemm_fused6_kernel's forms (math GCG_MATH_BF16X6): the weight split in every workgroup's
+    registers (no workspace; dense.FUSED_PRESPLIT off), the weight's planes pre-split into the
+    workspace on the 32-row 4-wave tile (tile 1) -- the same products in the same order: bitwise
+    equal (gradient, loss, hits, probabilities), rows past M included -- and on the 64-row 8-wave
+    tile (tile 2; tile 0 picks it at N > 768), whose row sums run over 8 column waves (another
+    association): within f32 rounding, the same hits."""
+    assert dense.tile_count("fused", "bf16x6") == 2
     P, W, b = _rand((M, K), 51, 0.3), _rand((K, N), 52, 0.3), _rand((N,), 53)
     y = np.random.default_rng(54).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
     yt = torch.from_numpy(y).to(cuda)
     Wp = dense.Projection().fwd.get(Wt, False)
 
-    def run(presplit, wr="1", wide="0", fx_narrow="0"):
+    def run(presplit, tile=0):
         monkeypatch.setattr(dense, "FUSED_PRESPLIT", presplit)
-        monkeypatch.setenv("GCG_FUSED6_WR", wr)
-        monkeypatch.setenv("GCG_FUSED6_WIDE", wide)
-        monkeypatch.setenv("GCG_FUSED6_FX_NARROW", fx_narrow)
         G = empty_dense(M, N, cuda)
         loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
-        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits)
+        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits, math="bf16x6", tile=tile)
         probs = empty_dense(M, N, cuda)
-        dense._fused(Pt, Wp, bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None)
+        dense._fused(Pt, Wp, bt, None, 1.0, None, probs, torch.empty(M, device=cuda), None,
+                     math="bf16x6", tile=tile)
         return G, loss, hits, probs
 
     ref = run(False)
-    for o in (run(False, wr="2"), run(True, fx_narrow="1")):
-        for a, r in zip(o, ref):
+    for a, r in zip(run(True, tile=1), ref):
+        assert torch.equal(a, r)
+    wide = [run(True)] + ([run(True, tile=2)] if N > 768 else [])
+    if N <= 768:  # tile 0 is the 32-row form there
+        for a, r in zip(wide[0], ref):
             assert torch.equal(a, r)
-    for o in (run(False, wide="1"), run(True)):
-        G2, l2, h2, p2 = o
+        from graphconvgeo_amd._native import NativeError
+        with pytest.raises(NativeError):
+            run(True, tile=2)  # the 64-row tile needs N > 768
+    for G2, l2, h2, p2 in wide:
         assert torch.equal(h2, ref[2])
         assert float((l2 - ref[1]).abs().max()) < 1e-5
         assert float((G2 - ref[0]).abs().max()) < 1e-6 / M + 1e-9
@@ -316,19 +316,19 @@ def test_gemm_tn_vs_float64(cuda, R, M, N):
     assert np.array_equal(C3, (C * np.float32(2.5)))
 
 
-@pytest.mark.parametrize("layout", ["1,2,8,1", "1,3,8,0", "1,2,8,0", "1,3,12,0", "1,1,8,4",
-                                    "1,3,3,0,2", "1,2,6,0,2"])
+@pytest.mark.parametrize("tile", [1, 2, 3, 4, 5, 6, 7])
 @pytest.mark.parametrize("R,M,N", [(4097, 300, 930), (70001, 256, 300), (513, 70, 129), (5, 3, 200)])
-def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, layout, monkeypatch):
-    """Every split-K wave layout (GCG_TN=MG,NG,PD,WM: workgroup tiles WM = 1, per-wave tiles
-    WM = 0 -- the default -- and waves stacked along M) against float64, with ragged R (steps
-    that end inside a split read zeros through the buffer range check), M and N off the tiles."""
-    monkeypatch.setenv("GCG_TN", layout)
+def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, tile):
+    """Every split-K wave layout (gcg_gemm_tn tiles 1..7: workgroup tiles WM = 1, per-wave tiles
+    WM = 0 -- the default family -- and waves stacked along M) against float64, with ragged R
+    (steps that end inside a split read zeros through the buffer range check), M and N off the
+    tiles."""
+    assert dense.tile_count("gemm_tn") == 7 and dense.tile_count("gemm_tn", "bf16x6") == -1
     A, B = _rand((R, M), 45, 0.5), _rand((R, N), 46, 0.5)
     At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
-    C = dense.gemm_tn(At, Bt).cpu().numpy()
+    C = dense.gemm_tn(At, Bt, tile=tile).cpu().numpy()
     _check_gemm(C, A.T.copy(), B)
-    assert np.array_equal(C, dense.gemm_tn(At, Bt).cpu().numpy())  # deterministic
+    assert np.array_equal(C, dense.gemm_tn(At, Bt, tile=tile).cpu().numpy())  # deterministic
 
 
 def test_gemm_tn_strided_views(cuda):
@@ -375,17 +375,18 @@ def test_side_stream_weight_grads_equal_inline(cuda, shared_w):
 @pytest.mark.parametrize("M,K,N", [(1, 1, 1), (65, 17, 5), (129, 300, 300), (200, 33, 320),
                                    (257, 64, 321), (130, 300, 512), (300, 300, 930),
                                    (77, 40, 1024), (100, 20, 1500), (64, 930, 300)])
-def test_lds_b_gemm_equals_register_b_gemm(cuda, M, K, N, monkeypatch):
-    """The plain products' default tiles (B staged through LDS, gemm_bl_kernel) accumulate in
-    the same k order as gemm_kernel (GCG_GEMM_BL=0): bitwise equal, bias + rectify included."""
+def test_lds_b_gemm_equals_register_b_gemm(cuda, M, K, N):
+    """The plain products' default tile (B staged through LDS, gemm_bl_kernel) accumulates in
+    the same k order as tile 1 (gemm_kernel, B straight to registers): bitwise equal, bias +
+    rectify included."""
     A, B, bias = _rand((M, K), M + 1), _rand((K, N), N + 2), _rand((N,), 3)
     At = torch.from_numpy(A).to(cuda)
     Bt = _padded(B, cuda)
     bt = torch.from_numpy(bias).to(cuda)
     outs = []
-    for knob in ("1", "0"):
-        monkeypatch.setenv("GCG_GEMM_BL", knob)
-        outs.append((dense.gemm(At, Bt), dense.gemm(At, Bt, bias=bt, act="relu")))
+    for tile in (0, 1):
+        outs.append((dense.gemm(At, Bt, tile=tile),
+                     dense.gemm(At, Bt, bias=bt, act="relu", tile=tile)))
     assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
     _check_gemm(outs[0][1].cpu().numpy(), A, B, bias, relu=True)
 
@@ -406,43 +407,35 @@ def test_gemm_nt_vs_float64(cuda, M, K, N, math):
     _check_gemm(C, A, B)
 
 
-@pytest.mark.parametrize("cfg", ["2,1,4,1,2,0", "2,1,4,1,2,1", "2,1,4,1,3,0", "2,1,4,1,3,1",
-                                 "1,1,4,1,2,0", "1,1,4,1,3,0", "3,1,4,1,2,0", "2,2,4,1,2,0",
-                                 "2,1,2,2,2,0", "4,1,4,1,2,0", "2,1,4,1,2,0,16",
-                                 "2,1,4,1,3,0,16", "2,1,4,1,4,0,16", "2,1,4,1,5,0,16",
-                                 "2,1,4,1,6,0,16", "4,1,4,1,4,0,16", "2,2,4,1,4,0,16",
-                                 "1,1,4,1,4,0,16", "1,1,4,1,6,0,16"])
-def test_gemm_nt_tile_variants(cuda, cfg, monkeypatch):
-    """Every instantiated tile (GCG_NT_CFG experiment knob) on ragged M / N / K, bias + relu."""
-    monkeypatch.setenv("GCG_NT_CFG", cfg)
+@pytest.mark.parametrize("tile", list(range(11)))
+def test_gemm_nt_tile_variants(cuda, tile):
+    """Every f32 NT tile (gcg_gemm_nt math GCG_MATH_F32, tiles 0..10) on ragged M / N / K, bias +
+    relu: within the float64 bar and bitwise equal to tile 0 (the same k order)."""
+    assert dense.tile_count("gemm_nt", "f32") == 10
     M, K, N = 333, 301, 133
     A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
-    C = dense.gemm_nt(torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True),
-                      bias=torch.from_numpy(b).to(cuda), act="relu", math="f32").cpu().numpy()
-    _check_gemm(C, A, B, bias=b, relu=True)
-
-
-NT3_TILES = ["2,1,4,1,2", "2,1,4,1,3", "4,1,4,1,2", "2,2,4,1,2", "2,2,4,1,3", "2,1,2,2,2",
-             "4,1,2,2,2", "2,1,4,2,2", "2,1,4,2,3", "2,2,4,2,2", "4,1,4,2,2", "2,1,4,1,0",
-             "2,2,4,1,0", "4,1,4,1,0", "2,1,2,1,0", "2,2,2,1,0", "4,1,2,1,0", "2,1,4,2,0",
-             "2,3,4,1,0", "2,3,2,1,0"]
+    At, Bt, bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True), torch.from_numpy(b).to(cuda)
+    C = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="f32", tile=tile)
+    _check_gemm(C.cpu().numpy(), A, B, bias=b, relu=True)
+    assert torch.equal(C, dense.gemm_nt(At, Bt, bias=bt, act="relu", math="f32"))
 
 
 @pytest.mark.parametrize("M,K,N", [(333, 301, 133), (1000, 300, 930), (517, 930, 300),
                                    (70, 33, 65), (1, 5, 3)])
-def test_gemm_nt_bf16x6_tiles_bitwise(cuda, M, K, N, monkeypatch):
-    """Every bf16x6 tile (GCG_NT3_CFG; S = 0: A in registers) and the in-loop split of both
-    operands accumulate the same six plane products in the same order: bitwise equal to each
-    other, with bias + relu, ragged M / N / K; within the float64 bar."""
+def test_gemm_nt_bf16x6_tiles_bitwise(cuda, M, K, N):
+    """Every bf16x6 tile (gcg_gemm_nt math GCG_MATH_BF16X6, tiles 0..8: A in registers or through
+    LDS) and the in-loop split of both operands accumulate the same six plane products in the
+    same order: bitwise equal to each other, with bias + relu, ragged M / N / K; within the
+    float64 bar."""
+    assert dense.tile_count("gemm_nt", "bf16x6") == 8
     A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
     At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
     bt = torch.from_numpy(b).to(cuda)
     ref = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6_inloop")
     _check_gemm(ref.cpu().numpy(), A, B, bias=b, relu=True)
-    for cfg in NT3_TILES:
-        monkeypatch.setenv("GCG_NT3_CFG", cfg)
-        C = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6")
-        assert torch.equal(C, ref), cfg
+    for tile in range(9):
+        C = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6", tile=tile)
+        assert torch.equal(C, ref), tile
 
 
 def test_gemm_nt_bf16x6_error_at_most_f32s(cuda):
@@ -479,21 +472,20 @@ def test_gemm_nt_bf16x6_nan_propagates(cuda):
 
 
 @pytest.mark.parametrize("math", dense.NT_MATHS)
-@pytest.mark.parametrize("tile", [None, "2,1,4,1,2", "2,2,4,1,0"])
-def test_gemm_nt_padding_never_leaks(cuda, math, tile, monkeypatch):
+@pytest.mark.parametrize("tile", [0, 2, 5])
+def test_gemm_nt_padding_never_leaks(cuda, math, tile):
     """The k tail is zeroed in the fragments: NaN in the operands' padding columns (k >= K, inside
-    the row stride) and in rows past M / N must not reach C."""
-    if tile is not None:
-        if math != "bf16x6":
-            pytest.skip("tile knob of the pre-split kernel")
-        monkeypatch.setenv("GCG_NT3_CFG", tile)
+    the row stride) and in rows past M / N must not reach C (bf16x6 tiles 2 / 5: A in
+    registers 128 x 128, A through LDS 128 x 64; f32 tiles 2 / 5: PF, 128 x 128)."""
+    if tile and math == "bf16x6_inloop":
+        pytest.skip("the in-loop split has one tile")
     M, K, N = 200, 298, 70
     A, B = _rand((M, K), 16), _rand((K, N), 17)
     Ap = torch.full((M, 300), float("nan"), device=cuda)
     Ap[:, :K] = torch.from_numpy(A).to(cuda)
     Btp = torch.full((N, 300), float("nan"), device=cuda)
     Btp[:, :K] = torch.from_numpy(B.T.copy()).to(cuda)
-    C = dense.gemm_nt(Ap[:, :K], Btp[:, :K], math=math).cpu().numpy()
+    C = dense.gemm_nt(Ap[:, :K], Btp[:, :K], math=math, tile=tile).cpu().numpy()
     assert np.isfinite(C).all()
     _check_gemm(C, A, B)
 
@@ -581,3 +573,96 @@ def test_weighted_softmax_xent_vs_float64(cuda, M, K, N):
     _P, lr64, hr64, Gr64 = O.softmax_xent_f64(L64, y, scale=1.0 / T)
     assert abs(float(lw) - (w * lr64).sum() / T) < 1e-5 * max(1.0, abs(float(lw)))
     assert np.abs(L.grad.cpu().numpy() - w[:, None] * Gr64).max() < 1e-5 * w.max() / T + 1e-7
+
+
+BF16_OVERFLOW = 3.3961e38  # |x| from here on rounds to Inf in bf16 (bf16 max + half an ulp)
+
+
+def _nonfinite_operands(M, K, N, seed):
+    """A, B with +-Inf, NaN, values past bf16's largest finite (|x| >= 3.3961e38 rounds plane 0
+    to Inf) and a row / column pair whose products overflow, each in its own rows / columns."""
+    A, B = _rand((M, K), seed), _rand((K, N), seed + 1)
+    A[3, 7] = np.inf
+    A[11, 0] = -np.inf
+    A[20, K - 1] = 3.4e38
+    A[29, 5] = -3.3999e38
+    B[9, 4] = np.inf
+    B[K - 2, 13] = 3.4e38
+    A[40, :] = 1e20                  # row 40 x column 50: every product 1e40 -> Inf in f32
+    B[:, 50] = 1e20
+    A[45, 2] = np.nan
+    return A, B
+
+
+@pytest.mark.parametrize("M,K,N", [(64, 100, 70), (300, 301, 133), (1000, 300, 930)])
+def test_gemm_nt_bf16x6_nonfinite_has_f32_semantics(cuda, M, K, N):
+    """gcg_spmm.h: a bf16x6 tile whose result is not finite is recomputed on the f32 MFMA in the
+    f32 kernel's k order. So an infinite operand gives +-Inf (not the planes' Inf - Inf = NaN),
+    an operand above bf16's largest finite value is not lost to a NaN, an overflow gives Inf,
+    NaN stays NaN: the rows / columns of such operands are bitwise the f32 kernel's, in every
+    bf16x6 form (tiles 0..8 with the plane workspace, and the in-loop split); every non-finite
+    output equals the f32 one; finite outputs within the float64 bar."""
+    A, B = _nonfinite_operands(M, K, N, 70)
+    bias = _rand((N,), 72)
+    At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
+    bt = torch.from_numpy(bias).to(cuda)
+    ref = dense.gemm_nt(At, Bt, bias=bt, math="f32").cpu().numpy()
+    assert np.isinf(ref).any() and np.isnan(ref).any()
+    special = lambda X: ~np.isfinite(X) | (np.abs(X) >= BF16_OVERFLOW)  # noqa: E731
+    bad_rows = np.unique(np.nonzero(special(A))[0])
+    bad_cols = np.unique(np.nonzero(special(B))[1])
+    with np.errstate(all="ignore"):
+        C64 = A.astype(np.float64) @ B.astype(np.float64) + bias
+        bound = 2e-6 * (np.abs(A).astype(np.float64) @ np.abs(B).astype(np.float64)
+                        + np.abs(bias)) + 1e-30
+    fin = np.isfinite(ref)
+    fin[bad_rows] = False
+    fin[:, bad_cols] = False
+    forms = [("bf16x6_inloop", 0)] + [("bf16x6", t) for t in range(9)]
+    for math, tile in forms:
+        C = dense.gemm_nt(At, Bt, bias=bt, math=math, tile=tile).cpu().numpy()
+        assert np.array_equal(np.isnan(C), np.isnan(ref)), (math, tile)
+        inf = np.isinf(ref)
+        assert np.array_equal(C[inf], ref[inf]), (math, tile)  # the sign of every Inf
+        assert np.array_equal(C[bad_rows], ref[bad_rows], equal_nan=True), (math, tile)
+        assert np.array_equal(C[:, bad_cols], ref[:, bad_cols], equal_nan=True), (math, tile)
+        assert (np.abs(C[fin] - C64[fin]) <= bound[fin]).all(), (math, tile)
+
+
+@pytest.mark.parametrize("N", [129, 930])
+def test_fused_bf16x6_nonfinite_has_f32_semantics(cuda, N):
+    """The fused output layer on the bf16 matrix cores against the f32 MFMA one, with an
+    infinite activation, a NaN, one past bf16's largest finite value (whose products all
+    overflow to -Inf) and one product that overflows to +Inf: the same non-finite losses and
+    gradient entries (NaN / Inf pattern) as the f32 kernel, every other row within f32
+    rounding. (Rows whose logits are finite but ~1e19 are avoided: exp(v - max) of such rows
+    is decided by the last rounding bit in either arithmetic.)"""
+    M, K = 70, 40
+    P, W = _rand((M, K), 81, 0.3), _rand((K, N), 82, 0.3)
+    b = _rand((N,), 83)
+    P[3, 5] = np.inf
+    P[17, 9] = np.nan
+    P[10, 1] = -3.4e38
+    W[1, :] = 2.0        # row 10: every product -6.8e38 -> -Inf
+    P[:, 2] = 0.0
+    P[33, 2] = 1e20
+    W[2, 7] = 1e20       # row 33 x column 7: 1e40 -> +Inf
+    y = np.random.default_rng(84).integers(0, N, M).astype(np.int32)
+    Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
+    yt = torch.from_numpy(y).to(cuda)
+    Wp = dense.Projection().fwd.get(Wt, False)
+    res = {}
+    for math in ("f32", "bf16x6"):
+        G = empty_dense(M, N, cuda)
+        loss, hits = torch.empty(M, device=cuda), torch.empty(M, device=cuda)
+        dense._fused(Pt, Wp, bt, yt, 1.0 / M, None, G, loss, hits, math=math)
+        res[math] = (G.cpu().numpy(), loss.cpu().numpy(), hits.cpu().numpy())
+    (Gf, lf, hf), (Gb, lb, hb) = res["f32"], res["bf16x6"]
+    special = [3, 10, 17, 33]
+    assert not np.isfinite(lf[special]).any()
+    assert np.array_equal(np.isnan(lb), np.isnan(lf)) and np.array_equal(np.isinf(lb), np.isinf(lf))
+    assert np.array_equal(np.isnan(Gb), np.isnan(Gf)) and np.array_equal(np.isinf(Gb), np.isinf(Gf))
+    fin = np.isfinite(lf)
+    assert fin.sum() == M - len(special)
+    assert np.abs(lb[fin] - lf[fin]).max() < 1e-5
+    assert np.abs(Gb[fin] - Gf[fin]).max() < 1e-6

@@ -1,6 +1,8 @@
 """GPU SpGEMM (input convolution X_conv = H * X, main.py:530 / tensormain.py:114) vs scipy."""
 import warnings
 
+import functools
+
 import numpy as np
 import pytest
 import scipy.sparse as sps
@@ -78,11 +80,10 @@ def test_spgemm_empty(cuda):
 
 
 @pytest.mark.parametrize("chunk", [1, 37, 1000, 50_000])
-def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
+def test_spgemm_row_chunks_bitwise(cuda, chunk):
     """Row-chunked expand-sort-reduce (products > int32 at Twitter-World scale): forcing tiny
     chunks -- single rows larger than a chunk, chunks of empty rows -- leaves C bitwise equal."""
-    monkeypatch.setenv("GCG_SPGEMM_ESC", "1")  # the expand-sort-reduce path
-    monkeypatch.setenv("GCG_SPGEMM_CHUNK", str(chunk))
+    sg = functools.partial(gs.spgemm, paths=("expand_sort",), chunk_products=chunk)
     rng = np.random.default_rng(chunk)
     A = sps.random(900, 400, density=0.03, random_state=3, format="lil", dtype=np.float32)
     A[100:220, :] = 0          # a block of empty rows
@@ -100,13 +101,13 @@ def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
     A = sps.lil_matrix(A)
     A[600, 1], A[600, 2] = 2.0, 2.0
     A = sps.csr_matrix(A)
-    C = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
+    C = sg(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
     ref = canon(A @ B)
     assert np.array_equal(C.indptr, ref.indptr)
     assert np.array_equal(C.indices, ref.indices)
     assert np.array_equal(C.data, ref.data)
     A64 = torch.as_tensor(A.data.astype(np.float64) * 1.0000001, device=cuda)
-    C64 = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda), a_data64=A64).to_scipy()
+    C64 = sg(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda), a_data64=A64).to_scipy()
     A64h = sps.csr_matrix((A64.cpu().numpy(), A.indices, A.indptr), shape=A.shape)
     ref64 = canon((A64h @ B.astype(np.float64)).astype(np.float32))
     assert np.array_equal(C64.indptr, ref64.indptr) and np.array_equal(C64.indices, ref64.indices)
@@ -115,13 +116,12 @@ def test_spgemm_row_chunks_bitwise(cuda, monkeypatch, chunk):
 
 @pytest.mark.parametrize("path", ["rows", "dense", "esc"])
 @pytest.mark.parametrize("p", [300, 30_000, 60_000])
-def test_spgemm_rows_kernel_shapes(cuda, monkeypatch, path, p):
+def test_spgemm_rows_kernel_shapes(cuda, path, p):
     """The row-wise kernels (small rows: LDS sort; large rows: dense LDS slabs) across their regimes: several column slabs
     (p > 25,600 f32 / 13,312 f64), rows with > 2,048 products (several staging windows) and
     > 1,024 nonzeros (several step blocks), B rows longer than a wave, empty rows of A and B,
     exact cancellations -- bitwise scipy, f32 and f64 accumulation, both SpGEMM paths."""
-    monkeypatch.setenv("GCG_SPGEMM_ESC", "1" if path == "esc" else "0")
-    monkeypatch.setenv("GCG_SPGEMM_NO_SMALL", "1" if path == "dense" else "0")  # every row on slabs
+    sg = functools.partial(gs.spgemm, paths={"rows": (), "dense": ("dense_slabs",), "esc": ("expand_sort",)}[path])
     rng = np.random.default_rng(p)
     m, n = 400, 3000
     A = sps.random(m, n, density=0.004, random_state=5, format="lil", dtype=np.float32)
@@ -145,30 +145,30 @@ def test_spgemm_rows_kernel_shapes(cuda, monkeypatch, path, p):
     A[7, 1000], A[7, 1001] = 0.5, 0.5
     A = sps.csr_matrix(A)
     Ad, Bd = gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)
-    C = gs.spgemm(Ad, Bd).to_scipy()
+    C = sg(Ad, Bd).to_scipy()
     ref = canon(A @ B)
     assert C[7, p - 1] == 0 and ref[7, p - 1] == 0
     assert np.array_equal(C.indptr, ref.indptr)
     assert np.array_equal(C.indices, ref.indices)
     assert np.array_equal(C.data, ref.data)
     a64 = torch.as_tensor(A.data.astype(np.float64) / 3.0, device=cuda)
-    C64 = gs.spgemm(Ad, Bd, a_data64=a64).to_scipy()
+    C64 = sg(Ad, Bd, a_data64=a64).to_scipy()
     A64 = sps.csr_matrix((a64.cpu().numpy(), A.indices, A.indptr), shape=A.shape)
     ref64 = canon((A64 @ B.astype(np.float64)).astype(np.float32))
     assert np.array_equal(C64.indptr, ref64.indptr) and np.array_equal(C64.indices, ref64.indices)
     assert np.array_equal(C64.data, ref64.data)
-    Cacc = gs.spgemm(Ad, Bd, accumulate_f64=True).to_scipy()  # f32 A, float64 sums
+    Cacc = sg(Ad, Bd, accumulate_f64=True).to_scipy()  # f32 A, float64 sums
     refacc = canon((A.astype(np.float64) @ B.astype(np.float64)).astype(np.float32))
     assert np.array_equal(Cacc.indices, refacc.indices) and np.array_equal(Cacc.data, refacc.data)
 
 
 @pytest.mark.parametrize("compact", ["inplace", "tmp"])
-def test_spgemm_compaction_forms(cuda, monkeypatch, compact):
+def test_spgemm_compaction_forms(cuda, compact):
     """C rows are computed at their product offsets inside c_idx/c_val and compacted there (row
     ranges whose destinations precede their sources), or through an nnz(C) temporary when that
     would take too many launches. Rows that merge nothing (in place), rows that merge a little
     (short ranges, single rows overlapping themselves) and rows that merge a lot, mixed."""
-    monkeypatch.setenv("GCG_SPGEMM_COMPACT_TMP", "1" if compact == "tmp" else "0")
+    sg = functools.partial(gs.spgemm, paths=("compact_temporary",) if compact == "tmp" else ())
     rng = np.random.default_rng(11)
     n, p = 3000, 5000
     # rows of A: first 500 rows one step each (no merging: in place), then rows of 2 steps
@@ -181,7 +181,7 @@ def test_spgemm_compaction_forms(cuda, monkeypatch, compact):
     A = sps.csr_matrix((rng.standard_normal(len(rows)).astype(np.float32), (rows, cols)), shape=(n, n))
     B = sps.random(n, p, density=0.01, random_state=6, format="csr", dtype=np.float32)
     B.data = rng.standard_normal(B.nnz).astype(np.float32)
-    C = gs.spgemm(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
+    C = sg(gs.DeviceCSR.from_scipy(A, cuda), gs.DeviceCSR.from_scipy(B, cuda)).to_scipy()
     ref = canon(A @ B)
     assert ref.nnz < int(np.diff(B.indptr)[A.indices].sum())  # some rows merged
     assert np.array_equal(C.indptr, ref.indptr)

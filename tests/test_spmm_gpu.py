@@ -64,12 +64,12 @@ def test_bitwise_vs_oracle(cuda, K, mode):
 
 @pytest.mark.parametrize("K", [1, 3, 63, 65, 129, 301, 513, 930])
 @pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
-def test_masked_tail_vec4_bitwise(cuda, K, mode, monkeypatch):
+def test_masked_tail_vec4_bitwise(cuda, K, mode):
     """K % 4 != 0 on rows padded to a multiple of 4 floats (empty_dense; C = 930 -> 960): dwordx4
-    gathers with a masked last vector (spmm.hip TL = 1). Bitwise equal to the narrower gathers
-    (GCG_SPMM_NO_TAIL=1) and to the oracle, with bias + rectify + gate bytes, a row subset with
-    duplicates, cooperative hub rows (ordered) and split rows (fast); Y's and the gate's padding
-    columns are never written."""
+    gathers with a masked last vector (spmm.hip TL = 1). Bitwise equal to the narrower gathers of
+    the same Z on unpadded rows (row stride K: dwordx2 / dword vectors) and to the oracle, with
+    bias + rectify + gate bytes, a row subset with duplicates, cooperative hub rows (ordered) and
+    split rows (fast); Y's and the gate's padding columns are never written."""
     H = rand_csr(700, 900, 12, seed=K, long_rows=[(5, 4500), (600, 1500)])
     Z = np.random.default_rng(K).standard_normal((900, K)).astype(np.float32)
     b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
@@ -78,23 +78,24 @@ def test_masked_tail_vec4_bitwise(cuda, K, mode, monkeypatch):
     A = gs.DeviceCSR.from_scipy(H, cuda)
     Zd = gs.empty_dense(900, K, cuda).copy_(to_dev(Z, cuda))
     Zd.as_strided((900, Zd.stride(0)), (Zd.stride(0), 1))[:, K:] = float("nan")  # padding
+    Zn = to_dev(Z, cuda).contiguous()  # row stride K: the narrow gathers
+    assert Zd.stride(0) % 4 == 0 and (K % 4 == 0 or Zn.stride(0) % 4 != 0)
     bd = to_dev(b, cuda)
     outs = {}
-    for no_tail in ("1", "0"):
-        monkeypatch.setenv("GCG_SPMM_NO_TAIL", no_tail)
+    for name, Zx in (("vec4", Zd), ("narrow", Zn)):
         Y = gs.empty_dense(700, K, cuda)
         Yfull = Y.as_strided((700, Y.stride(0)), (Y.stride(0), 1))
         Yfull.fill_(7.0)
         gate = gs.empty_gate(700, K, cuda)
         gfull = gate.as_strided((700, gate.stride(0)), (gate.stride(0), 1))
         gfull.fill_(9)
-        gs.spmm(A, Zd, bias=bd, act="relu", mode=mode, gate=gate, out=Y, task_nnz=256)
-        Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
+        gs.spmm(A, Zx, bias=bd, act="relu", mode=mode, gate=gate, out=Y, task_nnz=256)
+        Ys = gs.spmm(A, Zx, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
         assert torch.all(Yfull[:, K:] == 7.0) and torch.all(gfull[:, K:] == 9)
-        outs[no_tail] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
-    for a, c in zip(outs["0"], outs["1"]):
+        outs[name] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
+    for a, c in zip(outs["vec4"], outs["narrow"]):
         assert np.array_equal(a, c)
-    Y, gate, Ys = outs["0"]
+    Y, gate, Ys = outs["vec4"]
     if mode == "fast":
         assert np.abs(Y - O.spmm_f32(H, Z, bias=b, act="relu")).max() <= 1e-5
     else:
@@ -154,13 +155,12 @@ def test_bias_relu_and_rows_subset(cuda, mode):
 
 
 @pytest.mark.parametrize("K", [4, 16, 60, 64, 68, 96, 124, 128])
-@pytest.mark.parametrize("mode", ["rowwise", "ordered", "fast"])
-def test_narrow_rows_subwave_path(cuda, K, mode, monkeypatch):
-    """Narrow rows, 2 (K <= 128) or 4 (K <= 64) per wave, one lane group per row
-    (spmm_rows_kernel<4, 1, 16, 4, SUB>; the default takes it plan-less at K <= 96, forced here
-    in every mode): bitwise equal to the whole-wave path (GCG_SPMM_SUB=1) and to the oracle in
-    the bitwise modes, with bias + rectify + gate bytes, a row subset with duplicates, empty rows,
-    a cooperative hub row (ordered) and split rows (fast)."""
+def test_narrow_rows_subwave_path(cuda, K):
+    """Narrow rows: plan-less (rowwise) launches run 4 rows per wave at K <= 64 and 2 at K <= 96
+    (spmm_rows_kernel<4, 1, 16, 4, SUB>, one lane group per row); the planned modes run one row
+    per wave. Rowwise bitwise equal to ordered and to the oracle, with bias + rectify + gate
+    bytes, a row subset with duplicates, empty rows and a cooperative hub row (ordered); fast
+    (split rows) within 1e-5, bitwise on unsplit rows."""
     H = rand_csr(777, 600, 10, seed=11 + K, long_rows=[(9, 4100), (500, 700)], empty_frac=0.15)
     Z = np.random.default_rng(K).standard_normal((600, K)).astype(np.float32)
     b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
@@ -169,26 +169,23 @@ def test_narrow_rows_subwave_path(cuda, K, mode, monkeypatch):
     A = gs.DeviceCSR.from_scipy(H, cuda)
     Zd, bd = to_dev(Z, cuda), to_dev(b, cuda)
     outs = {}
-    for sub in ("4" if K <= 64 else "2", "1"):  # forced, so the planned modes take it too
-        monkeypatch.setenv("GCG_SPMM_SUB", sub)
+    for mode in ("rowwise", "ordered", "fast"):
         gate = gs.empty_gate(H.shape[0], K, cuda)
         Y = gs.spmm(A, Zd, bias=bd, act="relu", mode=mode, gate=gate, task_nnz=256)
         Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)
-        outs[sub] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
-    for a, c in zip(outs["4" if K <= 64 else "2"], outs["1"]):
+        outs[mode] = (Y.cpu().numpy(), gate.cpu().numpy(), Ys.cpu().numpy())
+    for a, c in zip(outs["rowwise"], outs["ordered"]):
         assert np.array_equal(a, c)
-    Y, gate, Ys = outs["1"]
+    Y, gate, Ys = outs["ordered"]
     ref = O.spmm_f32(H, Z, bias=b, act="relu")
     pre = O.spmm_f32(H, Z, bias=b)
-    refs = O.spmm_f32(H, Z, rows=rows)
-    if mode == "fast":
-        assert np.abs(Y - ref).max() <= 1e-5
-        unsplit = np.diff(H.indptr) <= 256
-        assert np.array_equal(Y[unsplit], ref[unsplit])
-    else:
-        assert np.array_equal(Y, ref) and np.array_equal(Ys, refs)
-        want = np.where(pre > 0, 2, np.where(pre == 0, 1, 0)).astype(np.uint8)
-        assert np.array_equal(gate, want)
+    assert np.array_equal(Y, ref) and np.array_equal(Ys, O.spmm_f32(H, Z, rows=rows))
+    want = np.where(pre > 0, 2, np.where(pre == 0, 1, 0)).astype(np.uint8)
+    assert np.array_equal(gate, want)
+    Yf = outs["fast"][0]
+    assert np.abs(Yf - ref).max() <= 1e-5
+    unsplit = np.diff(H.indptr) <= 256
+    assert np.array_equal(Yf[unsplit], ref[unsplit])
 
 
 @pytest.mark.parametrize("mode", ["ordered", "fast"])
@@ -212,7 +209,7 @@ def test_gather_hint_is_cache_policy_only(cuda, mode, K, monkeypatch):
     Zd = gs.empty_dense(20_000, K, cuda).copy_(to_dev(Z, cuda))
     outs = {}
     for off in ("0", "1"):
-        monkeypatch.setenv("GCG_SPMM_NO_HINT", off)
+        monkeypatch.setattr(gs, "GATHER_HINT", off == "0")  # "1": the hint-less launch
         gate = gs.empty_gate(20_000, K, cuda)
         Y = gs.spmm(A, Zd, bias=to_dev(b, cuda), act="relu", mode=mode, gate=gate, task_nnz=256)
         Ys = gs.spmm(A, Zd, rows=gs.RowSelection(rows, cuda), mode=mode, task_nnz=256)

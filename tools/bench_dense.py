@@ -49,8 +49,8 @@ def main():
     ap.add_argument("--hidden", type=int, default=300)
     ap.add_argument("--classes", type=int, default=930)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--tiles", default="rt2,rt4,8w,occ2", help="wide-tile variants to compare")
-    ap.add_argument("--tn", default="1:2:8,1:2:4,1:1:8,1:1:16", help="TN tile variants")
+    ap.add_argument("--tiles", default="1,2,3,4,5", help="f32 fused-layer tiles to compare")
+    ap.add_argument("--tn", default="1,2,3,6", help="gcg_gemm_tn tiles to compare")
     args = ap.parse_args()
     dev = torch.device("cuda:0")
     T, N, K, C = args.rows, args.nodes, args.hidden, args.classes
@@ -87,16 +87,10 @@ def main():
     def ours_fused():
         dense._fused(P, Wp, b, y32, 1.0 / T, None, G, loss, hits)
 
-    knobs = {"rt2": {"GCG_GEMM_RT": "2", "GCG_GEMM_OCC2": "0"},
-             "rt4": {"GCG_GEMM_RT": "4", "GCG_GEMM_OCC2": "0"},
-             "8w": {"GCG_GEMM_8W": "1"}, "occ2": {"GCG_GEMM_OCC2": "1"}}
-    for name in args.tiles.split(","):  # wide-tile variants (experiment knobs of dense.hip)
-        for k, v in knobs[name].items():
-            os.environ[k] = v
-        rec(f"proj P.W2+b2 {name}", time_op(lambda: dense.gemm(P, Wp, bias=b, out=out), args.reps), f)
-        rec(f"fused {name}", time_op(ours_fused, args.reps), f)
-        for k in knobs[name]:
-            os.environ.pop(k, None)
+    for tile in [int(t) for t in args.tiles.split(",") if t]:  # f32 fused tiles (B parts)
+        rec(f"fused f32 tile {tile}",
+            time_op(lambda: dense._fused(P, Wp, b, y32, 1.0 / T, None, G, loss, hits, math="f32",
+                                         tile=tile), args.reps), f)
     rec("proj P.W2+b2", time_op(lambda: dense.gemm(P, Wp, bias=b, out=out), args.reps), f,
         time_op(lambda: torch.addmm(b, P, W), args.reps))
 
@@ -115,10 +109,8 @@ def main():
     Gc = G
     rec("dP = G.W2^T", time_op(lambda: dense.gemm(Gc, Wt), args.reps), f,
         time_op(lambda: torch.matmul(Gc, W.t()), args.reps))
-    for tn in args.tn.split(","):  # split-K TN tile variants (GCG_TN=MG,NG,PD)
-        os.environ["GCG_TN"] = tn.replace(":", ",")
-        rec(f"dW2 = P^T.G tn={tn}", time_op(lambda: dense.gemm_tn(P, Gc), args.reps), f)
-    os.environ.pop("GCG_TN", None)
+    for tn in [int(t) for t in args.tn.split(",") if t]:  # split-K layouts (gcg_gemm_tn tiles)
+        rec(f"dW2 = P^T.G tile={tn}", time_op(lambda: dense.gemm_tn(P, Gc, tile=tn), args.reps), f)
     rec("dW2 = P^T.G", time_op(lambda: dense.gemm_tn(P, Gc), args.reps), f,
         time_op(lambda: torch.matmul(P.t(), Gc), args.reps))
     del G, Gc, out

@@ -10,7 +10,7 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from graphconvgeo_amd import sparse as gs  # noqa: E402
-from graphconvgeo_amd.distributed import RowPartitionedCSR  # noqa: E402
+from graphconvgeo_amd.distributed import PartitionPlan, RowPartitionedCSR  # noqa: E402
 from graphconvgeo_amd.synth import CONFIGS, synthetic_graph  # noqa: E402
 
 K = 300
@@ -34,8 +34,9 @@ def timed(fn, reps=10):
 
 for P in [int(x) for x in os.environ.get("PARTS", "1,2,4,8").split(",")]:
     worst = {}
+    plan = PartitionPlan(H, P)
     for r in range(P):
-        part = RowPartitionedCSR(H, r, P, dev, exchange="allgather")
+        part = RowPartitionedCSR(H, r, P, dev, exchange="allgather", plan=plan)
         operand = gs.empty_dense(part.operand_rows(), K, dev).normal_()
         Y = gs.empty_dense(part.n_local, K, dev)
         line = []

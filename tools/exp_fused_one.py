@@ -1,6 +1,6 @@
 #!/usr/bin/env python
 """Fused output layer timing (Twitter-World 840k x 300 x 930 and Twitter-US 270k x 300 x 256),
-outputs checked against float64 on sampled rows."""
+every (math, tile) of gcg_project_softmax_xent, outputs checked against float64 on sampled rows."""
 import json
 import os
 import sys
@@ -24,15 +24,14 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     G = empty_dense(T, C, dev)
     loss = torch.empty(T, device=dev)
     hits = torch.empty(T, device=dev)
-    f = lambda: dense._fused(P, Wp, b, y, 1.0 / T, None, G, loss, hits)  # noqa: E731
-    f()
     torch.cuda.synchronize()
     rows = torch.randint(0, T, (400,), generator=g, device=dev)
     logits64 = P[rows].double() @ W.double() + b.double()
     _, l64, h64, G64 = O.softmax_xent_f64(logits64.cpu().numpy(), y[rows].cpu().numpy(), scale=1.0 / T)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for split in ("0", "4", "8", "16"):
-      os.environ["GCG_GEMM_SPLIT"] = split
+    forms = [("bf16x6", t) for t in range(3 if C > 768 else 2)] + [("f32", t) for t in range(6)]
+    for math, tile in forms:
+      f = lambda: dense._fused(P, Wp, b, y, 1.0 / T, None, G, loss, hits, math=math, tile=tile)  # noqa: E731
       f()
       torch.cuda.synchronize()
       err = max(float(np.abs(G[rows].cpu().numpy() - G64).max()) * T,
@@ -45,5 +44,5 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
         e.record()
         torch.cuda.synchronize()
         res.append(round(2.0 * T * K * C / (s.elapsed_time(e) / 10) / 1e9, 1))
-      print(json.dumps({"shape": f"{T}x{K}x{C}", "split": split, "TFLOPs": res, "max_err": err}),
+      print(json.dumps({"shape": f"{T}x{K}x{C}", "math": math, "tile": tile, "TFLOPs": res, "max_err": err}),
             flush=True)

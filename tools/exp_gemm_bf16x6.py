@@ -2,7 +2,7 @@
 """NT GEMM products on the bf16 matrix cores (gcg_gemm_nt_f32_bf16x6: three bf16 planes per f32
 operand, six plane products) against the f32-MFMA NT kernel (gcg_gemm_nt_f32) on the
 output-layer shapes: projection h.W2 (M x 300 x C) and input gradient g.W2^T (M x C x 300).
-Tile variants of the pre-split kernel via GCG_NT3_CFG; the in-loop split of both operands
+Tile variants of the pre-split kernel via gcg_gemm_nt's tile argument (1..8); the in-loop split of both operands
 (no workspace) as bf16x6_inloop. HIP events, mean of `reps`, interleaved rounds; error on 512
 sampled rows against float64, absolute and relative to sum_k |a||b| (the f32 rounding scale)."""
 import argparse
@@ -34,7 +34,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--rounds", type=int, default=2)
-    ap.add_argument("--cfgs", default="2,1,4,1,2;2,2,4,1,2;2,1,4,2,2;2,1,4,1,0;2,2,4,1,0;4,1,4,1,0;2,1,2,1,0;2,2,2,1,0;4,1,2,1,0;2,1,4,2,0")
+    ap.add_argument("--cfgs", default="0;1;2;3;4;5;6;7;8",
+                    help="gcg_gemm_nt bf16x6 tiles (0 = the default for the shape)")
     ap.add_argument("--shapes", default="840000x300x930,840000x930x300,1400000x300x930,"
                                         "450000x300x256,450000x256x300")
     args = ap.parse_args()
@@ -57,21 +58,16 @@ def main():
             d = np.abs(C[rows].double().cpu().numpy() - ref)
             return float(d.max()), float((d / scale).max())
 
-        variants = [("f32", None), ("bf16x6_inloop", None), ("bf16x6", None)] + [
-            ("bf16x6", c) for c in args.cfgs.split(";") if c]
+        variants = [("f32", 0), ("bf16x6_inloop", 0)] + [
+            ("bf16x6", int(c)) for c in args.cfgs.split(";") if c]
         for rnd in range(args.rounds):
             for math, cfg in variants:
-                if cfg is None:
-                    os.environ.pop("GCG_NT3_CFG", None)
-                else:
-                    os.environ["GCG_NT3_CFG"] = cfg
-                key = math if cfg is None else f"{math}[{cfg}]"
-                dense.gemm_nt(A, Wt, out=C, math=math)
+                key = f"{math}[{cfg}]"
+                dense.gemm_nt(A, Wt, out=C, math=math, tile=cfg)
                 if rnd == 0:
                     rec[f"err_abs[{key}]"], rec[f"err_rel[{key}]"] = err(C)
-                t = timeit(lambda: dense.gemm_nt(A, Wt, out=C, math=math), args.reps)
+                t = timeit(lambda: dense.gemm_nt(A, Wt, out=C, math=math, tile=cfg), args.reps)
                 rec.setdefault(f"TF[{key}]", []).append(round(flop / t / 1e9, 1))
-        os.environ.pop("GCG_NT3_CFG", None)
         print(json.dumps(rec), flush=True)
         del A, W, Wt, C
 

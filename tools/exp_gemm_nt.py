@@ -31,7 +31,8 @@ def timeit(fn, reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--cfgs", default="2,1,4,1,2,0;2,1,4,1,2,1;2,1,4,1,3,0;2,1,4,1,3,1;1,1,4,1,2,0;1,1,4,1,3,0;3,1,4,1,2,0;2,2,4,1,2,0;2,1,2,2,2,0;4,1,4,1,2,0")
+    ap.add_argument("--cfgs", default="0;1;2;3;4;5;6;7;8;9;10",
+                    help="gcg_gemm_nt f32 tiles")
     ap.add_argument("--shapes", default="840000x300x930,1400000x300x930,840000x930x300,"
                                         "1400000x930x300,450000x300x256,450000x256x300")
     args = ap.parse_args()
@@ -51,14 +52,13 @@ def main():
         rec["hipblaslt"] = round(flop / t / 1e9, 1)
         t = timeit(lambda: dense.gemm(A, Wp), args.reps)
         rec["gemm_f32"] = round(flop / t / 1e9, 1)
-        for cfg in args.cfgs.split(";"):
-            os.environ["GCG_NT_CFG"] = cfg
-            C = dense.gemm_nt(A, Wt)
+        for cfg in args.cfgs.split(";"):  # f32 tiles of gcg_gemm_nt (0..10)
+            tile = int(cfg)
+            C = dense.gemm_nt(A, Wt, math="f32", tile=tile)
             err = float(np.abs(C[rows].cpu().numpy() - ref).max())
-            t = timeit(lambda: dense.gemm_nt(A, Wt, out=C), args.reps)
+            t = timeit(lambda: dense.gemm_nt(A, Wt, out=C, math="f32", tile=tile), args.reps)
             rec[f"nt[{cfg}]"] = round(flop / t / 1e9, 1)
             rec[f"err[{cfg}]"] = err
-        os.environ.pop("GCG_NT_CFG", None)
         print(json.dumps(rec), flush=True)
         del A, W, Wp, Wt
 

@@ -1,7 +1,6 @@
 #!/usr/bin/env python
 """Profiling driver for rocprofv3 --pmc passes: 3 launches of the bench's SpMM (Twitter-World
-H . Z, K = 300) on the power-law or the uniform graph in the given mode (default ordered), optionally with non-temporal Y
-stores (GCG_SPMM_NT_STORE=1)."""
+H . Z, K = 300) on the power-law or the uniform graph in the given mode (default ordered)."""
 import os
 import sys
 
