@@ -39,6 +39,7 @@ SIGNATURES = {
     "gcg_spmm_plan_destroy": (C.c_int, [_p]),
     "gcg_spmm_plan_workspace_bytes": (C.c_int, [_p, _i64, _psz]),
     "gcg_spmm_plan_info": (C.c_int, [_p, _pi64, _pi64, _pi64, _pi64]),
+    "gcg_spmm_plan_hub_rows": (C.c_int, [_p, _pi64, _pi64, _pi64]),
     "gcg_spmm_csr_f32_planned": (C.c_int, [_p, _p, _p, _p, _p, _i64, _i64, _p, _i64, _p,
                                            C.c_int, _p, C.c_size_t, _p]),
     "gcg_spmm_csr_f32_gate": (C.c_int, [_i64, _i64, _i64, _p, _p, _p, _p, _i64, _i64, _p, _i64,

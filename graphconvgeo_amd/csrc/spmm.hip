@@ -326,29 +326,18 @@ __device__ __forceinline__ void lds_handover_barrier() {
 // the one the single-wave loop makes, in the same order: bitwise equal (scipy csr_matvecs).
 // A wave issues its next batch's gathers right after its own hand-over, so they fly while the
 // later waves of this batch add. LDS: one row sum (<= 512 floats).
-template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
-__device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
-                                         const int32_t* __restrict__ indices,
+//
+// coop_sum adds nonzeros [s, e) of one row to the running sum held in sacc (zero at the
+// row's first nonzero), gathering the columns gcol of each Z row: products v * Z[col] rounded,
+// then added (as acc + v * z without FMA).
+template <int VEC, int NCH, int U, int WPB, int HC>
+__device__ __forceinline__ void coop_sum(int s, int e, const int32_t* __restrict__ indices,
                                          const float* __restrict__ vals,
-                                         const int32_t* __restrict__ out_rows,
                                          const float* __restrict__ Z, int64_t ldz,
-                                         const int (&col)[NCH], const int (&gcol)[NCH],
-                                         const bool (&on)[NCH], int K, float* __restrict__ Y,
-                                         int64_t ldy, const float* __restrict__ bias, int act,
-                                         uint8_t* __restrict__ gate, int64_t ldgate,
-                                         float* __restrict__ sacc) {
+                                         const int (&gcol)[NCH], float* __restrict__ sacc) {
   const int wave = uniform(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & (kWave - 1);
-  const int r = out_rows ? uniform(out_rows[p]) : p;
-  const int s = uniform(indptr[r]);
-  const int e = uniform(indptr[r + 1]);
   constexpr int B = WPB * U;  // nonzeros per batch
-  if (wave == 0) {
-#pragma unroll
-    for (int k = 0; k < NCH; ++k)
-#pragma unroll
-      for (int q = 0; q < VEC; ++q) sacc[(k * kWave + lane) * VEC + q] = 0.0f;
-  }
   // (col, val) of this wave's nonzeros of a batch: one VECTOR load per wave (lane u holds
   // nonzero u, indices clamped into the row -- coop rows are never empty), prefetched one batch
   // ahead and moved to SGPRs with readlane when the batch is gathered. (Scalar-loaded pairs,
@@ -368,7 +357,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       c[u] = __builtin_amdgcn_readlane(ci, u);
-      if constexpr (HC) c[u] &= 0x7fffffff;  // experiment: strip the cold-column bit
+      if constexpr (HC) c[u] &= 0x7fffffff;  // the gather hint's cold-column bit
       v[u] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, vi), u));
     }
 #pragma unroll
@@ -442,7 +431,26 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
       lds_handover_barrier();
     }
   }
-  if (wave != 0) return;
+}
+
+template <int VEC, int NCH>
+__device__ __forceinline__ void sacc_fill(float* __restrict__ sacc, const float* __restrict__ src,
+                                          const int (&gcol)[NCH]) {
+  const int lane = threadIdx.x & (kWave - 1);
+#pragma unroll
+  for (int k = 0; k < NCH; ++k)
+    *reinterpret_cast<Vec<VEC>*>(sacc + (k * kWave + lane) * VEC) =
+        src ? load_vec<VEC>(src + gcol[k]) : Vec<VEC>{};
+}
+
+// bias, gate, rectify and the output row of a whole-workgroup row (wave 0)
+template <int VEC, int NCH, int TL>
+__device__ __forceinline__ void coop_epilogue(int p, const float* __restrict__ sacc,
+                                              const int (&col)[NCH], const bool (&on)[NCH], int K,
+                                              float* __restrict__ Y, int64_t ldy,
+                                              const float* __restrict__ bias, int act,
+                                              uint8_t* __restrict__ gate, int64_t ldgate) {
+  const int lane = threadIdx.x & (kWave - 1);
   float* yrow = Y + static_cast<int64_t>(p) * ldy;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
@@ -460,6 +468,81 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
   }
 }
 
+template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
+__device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
+                                         const int32_t* __restrict__ indices,
+                                         const float* __restrict__ vals,
+                                         const int32_t* __restrict__ out_rows,
+                                         const float* __restrict__ Z, int64_t ldz,
+                                         const int (&col)[NCH], const int (&gcol)[NCH],
+                                         const bool (&on)[NCH], int K, float* __restrict__ Y,
+                                         int64_t ldy, const float* __restrict__ bias, int act,
+                                         uint8_t* __restrict__ gate, int64_t ldgate,
+                                         float* __restrict__ sacc) {
+  const int r = out_rows ? uniform(out_rows[p]) : p;
+  const int s = uniform(indptr[r]);
+  const int e = uniform(indptr[r + 1]);
+  if (uniform(static_cast<int>(threadIdx.x >> 6)) == 0) sacc_fill<VEC, NCH>(sacc, nullptr, gcol);
+  coop_sum<VEC, NCH, U, WPB, HC>(s, e, indices, vals, Z, ldz, gcol, sacc);
+  if (uniform(static_cast<int>(threadIdx.x >> 6)) != 0) return;
+  coop_epilogue<VEC, NCH, TL>(p, sacc, col, on, K, Y, ldy, bias, act, gate, ldgate);
+}
+
+// Column-sliced hub rows (round 5). One CU's ordered sum of a hub row is bound by the rows it
+// has in flight (~19 GB/s for 1216-B random rows: 0.66 ms for a 12k-nonzero row of a P = 8
+// World block, longer than the rest of that block's launch). The columns are independent, so
+// a row of a two-chunk launch (NCH = 2) is cut into two column slices, each a whole-workgroup
+// task on its own CU that runs coop_sum over ALL the row's nonzeros for its half of the
+// columns: every column's additions are the single-wave loop's, in storage order (bitwise).
+// Half the floats per gathered row let a wave keep twice the rows in flight (U x NCH rows of
+// one chunk in the same registers), so each slice streams its row in half the time. (A
+// chained design -- row chunks on several CUs handing the running sum over through a flag
+// -- was built and measured first: 1.66 ms for the P = 8 block vs 1.04 whole-row, its phase
+// that adds stored products being as latency-bound as the gather)
+// Task {position, slice, -4, slices}. Launches of one chunk (NCH = 1: K <= 256 at dwordx4)
+// gain nothing from a slice, and the wider-chunk dword / dwordx2 launches (rows whose stride is
+// not a multiple of 4 floats) are not cut: slice 0 runs the whole row (coop_row), others exit.
+template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
+__device__ __forceinline__ void coop_slice(int p, int sl, int n_sl,
+                                           const int32_t* __restrict__ indptr,
+                                           const int32_t* __restrict__ indices,
+                                           const float* __restrict__ vals,
+                                           const int32_t* __restrict__ out_rows,
+                                           const float* __restrict__ Z, int64_t ldz,
+                                           const int (&col)[NCH], const int (&gcol)[NCH],
+                                           const bool (&on)[NCH], int K, float* __restrict__ Y,
+                                           int64_t ldy, const float* __restrict__ bias, int act,
+                                           uint8_t* __restrict__ gate, int64_t ldgate,
+                                           float* __restrict__ sacc) {
+  if constexpr (NCH != 2) {
+    if (sl == 0)
+      coop_row<VEC, NCH, U, WPB, HC, TL>(p, indptr, indices, vals, out_rows, Z, ldz, col, gcol,
+                                         on, K, Y, ldy, bias, act, gate, ldgate, sacc);
+  } else {
+    constexpr int US = U * NCH > kWave ? kWave : U * NCH;  // rows in flight per wave
+    const int lane = threadIdx.x & (kWave - 1);
+    const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
+    const int wp = min(kWave * VEC * NCH, K - panel0);                // panel width (floats)
+    const int ws = min(kWave * VEC, ((wp + n_sl - 1) / n_sl + VEC - 1) / VEC * VEC);
+    const int c0 = panel0 + sl * ws;
+    const int c1 = min(c0 + ws, panel0 + wp);
+    if (c0 >= c1) return;  // an empty slice (narrow last panel)
+    int scol[1], sgcol[1];
+    bool son[1];
+    scol[0] = c0 + lane * VEC;
+    son[0] = scol[0] < c1;
+    sgcol[0] = son[0] ? scol[0] : c0;
+    const int r = out_rows ? uniform(out_rows[p]) : p;
+    const int s = uniform(indptr[r]);
+    const int e = uniform(indptr[r + 1]);
+    const int wave = uniform(static_cast<int>(threadIdx.x >> 6));
+    if (wave == 0) sacc_fill<VEC, 1>(sacc, nullptr, sgcol);
+    coop_sum<VEC, 1, US, WPB, HC>(s, e, indices, vals, Z, ldz, sgcol, sacc);
+    if (wave != 0) return;
+    coop_epilogue<VEC, 1, TL>(p, sacc, scol, son, K, Y, ldy, bias, act, gate, ldgate);
+  }
+}
+
 // Main kernel. One wave per task; grid.y = column panel.
 //   tasks == nullptr : task w = rows of positions [w, w+1)           (plan-less path)
 //   task.w <  0      : rows of positions [task.x, task.y)            (short rows)
@@ -467,7 +550,9 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 // The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
 // (coop_row); the other tasks one wave each, in the blocks after them.
 template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0, int TL = 0>
-__global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
+// waves_per_eu(3): the K = 300 variant (VEC 4 x NCH 2, U = 16) otherwise lands one VGPR past
+// three waves per SIMD (169) once coop_slice's deeper batch is inlined beside the bulk path.
+__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(3))) void spmm_rows_kernel(
     const int4* __restrict__ tasks, int n_tasks, int n_coop, int n_out,
     const int32_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
@@ -488,11 +573,17 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     on[k] = col[k] < K;
     gcol[k] = on[k] ? col[k] : panel0;
   }
-  if (blk < n_coop) {  // a whole-workgroup long row (uniform across the block)
+  if (blk < n_coop) {  // a whole-workgroup long row or slice of one (uniform across the block)
     __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
-    coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z,
-                                       ldz, col, gcol, on, K, Y, ldy, bias, act, gate, ldgate,
-                                       sacc);
+    const int4 t0 = tasks[blk];
+    if (uniform(t0.z) == -4) {  // {position, slice, -4, slices}
+      coop_slice<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), uniform(t0.y), uniform(t0.w), indptr,
+                                           indices, vals, out_rows, Z, ldz, col, gcol, on, K, Y,
+                                           ldy, bias, act, gate, ldgate, sacc);
+    } else {
+      coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), indptr, indices, vals, out_rows, Z, ldz,
+                                         col, gcol, on, K, Y, ldy, bias, act, gate, ldgate, sacc);
+    }
     return;
   }
   const int w = uniform(n_coop + (blk - n_coop) * WPB + (threadIdx.x >> 6));
@@ -807,8 +898,13 @@ struct HostPlan {
   std::vector<int32_t> longs;  // quadruples
   int64_t n_slots = 0;
   int64_t max_task_nnz = 0;
-  int64_t n_coop = 0;  // leading tasks that are whole-workgroup rows (ordered mode)
+  int64_t n_coop = 0;        // leading whole-workgroup tasks: column slices, then whole rows
+  int64_t n_coop_rows = 0;   // rows on whole workgroups (sliced or not)
+  int64_t n_sliced = 0;      // ... of which cut into column slices (coop_slice)
 };
+
+// Column slices per whole-workgroup row (ordered == 1; ordered == 2 keeps whole rows)
+constexpr int kHubSlices = 2;
 
 // 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
 // long rows stay single-wave tasks scheduled first: 8 x task_nnz (4096 at Twitter-World). Measured (World power-law,
@@ -837,6 +933,8 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   hp->n_slots = 0;
   hp->max_task_nnz = 0;
   hp->n_coop = 0;
+  hp->n_coop_rows = 0;
+  hp->n_sliced = 0;
   const int64_t coop_min = coop_min_nnz(task_nnz);
   std::vector<int32_t> seg_tasks;
   std::vector<std::pair<int64_t, int64_t>> long_rows;  // (nnz, position), ordered mode
@@ -851,9 +949,11 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
     cur_cost = 0;
     cur_nnz = 0;
   };
+  int64_t work = 0;  // nonzeros of the output rows
   for (int64_t p = 0; p < n_out; ++p) {
     const int64_t r = out_rows ? out_rows[p] : p;
     if (r < 0 || r >= n_rows) return fail(GCG_ERR_INVALID_ARG, "out_rows[%lld]=%lld out of range", (long long)p, (long long)r);
+    work += indptr[r + 1] - indptr[r];
     const int64_t s = indptr[r], e = indptr[r + 1], len = e - s;
     if (!ordered && len > task_nnz) {
       close(p);
@@ -890,12 +990,21 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   std::stable_sort(coop_rows.begin(), coop_rows.end(), longest_first);
   std::stable_sort(long_rows.begin(), long_rows.end(), longest_first);
   std::vector<int32_t> head;
-  head.reserve((coop_rows.size() + long_rows.size()) * 4 + seg_tasks.size());
-  for (const auto& lr : coop_rows) {  // whole-workgroup rows: always the leading tasks
-    head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -2, -1});
+  head.reserve((coop_rows.size() * kHubSlices + long_rows.size()) * 4 + seg_tasks.size());
+  // whole-workgroup rows first, longest first: the column slices of every row (ordered == 1),
+  // or the whole row on one workgroup (ordered == 2: A/B and tests)
+  for (const auto& lr : coop_rows) {
+    if (ordered == 1) {
+      for (int k = 0; k < kHubSlices; ++k)
+        head.insert(head.end(), {int32_t(lr.second), k, -4, kHubSlices});
+      ++hp->n_sliced;
+    } else {
+      head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -2, -1});
+    }
     hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
   }
-  hp->n_coop = static_cast<int64_t>(coop_rows.size());
+  hp->n_coop_rows = static_cast<int64_t>(coop_rows.size());
+  hp->n_coop = hp->n_coop_rows + hp->n_sliced * (kHubSlices - 1);
   for (const auto& lr : long_rows) {
     head.insert(head.end(), {int32_t(lr.second), int32_t(lr.second + 1), -1, -1});
     hp->max_task_nnz = std::max(hp->max_task_nnz, lr.first);
@@ -913,7 +1022,7 @@ struct gcg_spmm_plan {
   int64_t n_rows = 0, n_cols = 0, nnz = 0, n_out = 0;
   int ordered = 0;
   int64_t task_nnz = 0;
-  int n_tasks = 0, n_long = 0, n_coop = 0;
+  int n_tasks = 0, n_long = 0, n_coop = 0, n_coop_rows = 0, n_sliced = 0;
   int64_t n_slots = 0, max_task_nnz = 0;
   int4* tasks = nullptr;     // device
   int4* longs = nullptr;     // device
@@ -1016,6 +1125,8 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
   p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
   p->n_long = static_cast<int>(hp.longs.size() / 4);
   p->n_coop = static_cast<int>(hp.n_coop);
+  p->n_coop_rows = static_cast<int>(hp.n_coop_rows);
+  p->n_sliced = static_cast<int>(hp.n_sliced);
   p->n_slots = hp.n_slots;
   p->max_task_nnz = hp.max_task_nnz;
   auto cleanup = [&]() { gcg_spmm_plan_destroy(p); };
@@ -1047,6 +1158,7 @@ gcg_status gcg_spmm_plan_destroy(gcg_spmm_plan* plan) {
 gcg_status gcg_spmm_plan_workspace_bytes(const gcg_spmm_plan* plan, int64_t K, size_t* bytes) {
   if (plan == nullptr || bytes == nullptr || K < 0) return fail(GCG_ERR_INVALID_ARG, "bad args");
   // Row stride rounded up to 4 floats so the workspace never forces a narrower vector width.
+  // One row per split-row segment (fast mode; ordered plans need none).
   const int64_t ldws = (K + 3) & ~int64_t{3};
   *bytes = static_cast<size_t>(plan->n_slots) * ldws * sizeof(float);
   return GCG_OK;
@@ -1056,9 +1168,19 @@ gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64
                               int64_t* n_segments, int64_t* max_task_nnz) {
   if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
   if (n_tasks) *n_tasks = plan->n_tasks;
-  if (n_long_rows) *n_long_rows = plan->n_long + plan->n_coop;  // split (fast) + whole-workgroup rows (ordered)
+  // split (fast) + whole-workgroup rows (ordered)
+  if (n_long_rows) *n_long_rows = plan->n_long + plan->n_coop_rows;
   if (n_segments) *n_segments = plan->n_slots;
   if (max_task_nnz) *max_task_nnz = plan->max_task_nnz;
+  return GCG_OK;
+}
+
+gcg_status gcg_spmm_plan_hub_rows(const gcg_spmm_plan* plan, int64_t* n_coop_rows,
+                                  int64_t* n_sliced_rows, int64_t* n_slices) {
+  if (plan == nullptr) return fail(GCG_ERR_INVALID_ARG, "plan is NULL");
+  if (n_coop_rows) *n_coop_rows = plan->n_coop_rows;
+  if (n_sliced_rows) *n_sliced_rows = plan->n_sliced;
+  if (n_slices) *n_slices = kHubSlices;
   return GCG_OK;
 }
 

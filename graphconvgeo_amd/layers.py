@@ -265,6 +265,58 @@ class SparseConvolutionDenseLayer(GraphConvLayer):
                          nonlinearity=nonlinearity, require_sparse_input=True, **kw)
 
 
+class _TransformPropagate(torch.autograd.Function):
+    """Y = (H . (h . W) + b)[rows]: ConvolutionDenseLayer in the reference order (mlpconv.py:
+    88-94) with a backward re-associated for the wide output (round 5).
+
+    Forward exactly as the reference associates it: Z = h . W on the NT GEMM (T.dot(h, W)),
+    then the C-wide SpMM (S.dot(H, Z) + b)[rows]. Theano's backward goes through the C-wide
+    dZ = H[rows]^T . g -- a C-wide transpose SpMM, then dh = dZ . W^T and dW = h^T . dZ over
+    every node. The same linear maps, re-associated:
+        dh = H[rows]^T . (g . W^T)      the NT GEMM over the target rows only, the SpMM K wide
+        dW = (H[rows] . h)^T . g        a K-wide SpMM over the target rows, the split-K
+                                        reduction over the target rows only (side stream)
+        db = colsum(g)
+    Equal in exact arithmetic; in fp32 within the same float64 bars as the reference
+    association (tests/test_config3_gpu.py, test_layers_gpu.py). Used when C > K (World: C =
+    930, K = 300: two K-wide SpMMs over the targets' nonzeros instead of one C-wide)."""
+
+    @staticmethod
+    def forward(ctx, h, W, b, H: gs.DeviceCSR, rows, mode, slot, proj):
+        Z = dense.gemm_nt(h, proj.fwd.get(W, True))  # T.dot(h, W), mlpconv.py:88
+        Y = gs.spmm(H, Z, bias=None if b is None else b.detach(), rows=rows, mode=mode)
+        ctx.save_for_backward(h, W)
+        ctx.H, ctx.rows, ctx.mode, ctx.slot, ctx.proj = H, rows, mode, slot, proj
+        ctx.has_b = b is not None
+        return Y
+
+    @staticmethod
+    def backward(ctx, g):
+        h, W = ctx.saved_tensors
+        H, rows, mode = ctx.H, ctx.rows, ctx.mode
+        g = g if g.stride(-1) == 1 else g.contiguous()
+        gh = gW = gb = None
+        if ctx.has_b and ctx.needs_input_grad[2]:
+            gb = dense._colsum(g)
+        if ctx.needs_input_grad[1]:
+            P = gs.spmm(H, h, rows=rows, mode=mode)  # (H . h)[rows], K wide
+            if ctx.slot is not None:  # the split-K reduction on the side stream
+                ctx.slot.args = (P, g, None)
+                gW = dense._placeholder_grad(W, g)
+            else:
+                gW = dense.gemm_tn(P, g)
+        if ctx.needs_input_grad[0]:
+            GW = dense.gemm_nt(g, ctx.proj.bwd.get(W, False))  # g . W^T over the target rows
+            T = H.rows_transpose(rows) if rows is not None else None
+            gh = gs.spmm(T, GW, mode=mode) if T is not None else H.tmatmul(GW, mode=mode)
+        return gh, gW, gb, None, None, None, None, None
+
+
+# reference order, C > K: the re-associated backward of _TransformPropagate (False: autograd
+# through dense.matmul + csr_matmul, Theano's association -- A/B and tests)
+REASSOCIATED_BACKWARD = True
+
+
 class ConvolutionDenseLayer(GraphConvLayer):
     """mlpconv.py:79-95: nonlinearity((S.dot(H, T.dot(h, W)) + b)[target_indices]).
 
@@ -298,7 +350,19 @@ class ConvolutionDenseLayer(GraphConvLayer):
         return csr_matmul(self.H, input, None, None, rows, self.mode)
 
     def forward(self, input, target_indices=None, **kwargs):
-        if self.order == "reference" or isinstance(input, gs.DeviceCSR) or sps.issparse(input):
+        sparse_in = isinstance(input, gs.DeviceCSR) or sps.issparse(input)
+        if (self.order == "reference" and not sparse_in and REASSOCIATED_BACKWARD
+                and self.fused_act is None and self.num_units > self.num_inputs
+                and torch.is_grad_enabled() and not torch.compiler.is_compiling()):
+            rows = None
+            if target_indices is not None:
+                rows = target_indices if isinstance(target_indices, gs.RowSelection) else \
+                    gs.RowSelection(target_indices, self.device)
+            proj = dense.projection_of(self.W)
+            Wa, slot = dense._weight_on_side_stream(self.W)
+            Y = _TransformPropagate.apply(input, Wa, self.b, self.H, rows, self.mode, slot, proj)
+            return self.post(Y) if self.post is not None else Y
+        if self.order == "reference" or sparse_in:
             return super().forward(input, target_indices=target_indices, **kwargs)
         P = self.propagate(input, target_indices)  # (H . h)[rows], K wide
         Y = dense.matmul(P, self.W, self.b)

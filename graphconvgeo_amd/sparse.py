@@ -82,6 +82,9 @@ TMATMUL_HEAD_SIDE_STREAM = True
 # mean: 15.5 MiB); every row non-temporal 7.71 vs 6.54; the uniform graphs have no column at
 # 4 x the mean (no hint). K = 256: 4.96 (16 MB) / 5.10 (32 MB) vs 5.36 ms, K = 128: 2.36 vs 2.43.
 GATHER_HINT = True
+# The plan of 'ordered' launches: 1 (whole-workgroup hub rows cut into two column slices on two
+# CUs, spmm.hip coop_slice) or 2 (every whole-workgroup row on one CU).
+ORDERED_PLAN = 1
 GATHER_HINT_HOT_BYTES = 32 << 20
 GATHER_HINT_MIN_REUSE = 4.0
 GATHER_HINT_MIN_SHARE = 0.25
@@ -178,12 +181,12 @@ def _destroy_retired_plans():
 class Plan:
     """Owning wrapper of a gcg_spmm_plan (nnz-balanced task list for one CSR + rows)."""
 
-    def __init__(self, A: "DeviceCSR", rows: Optional[RowSelection], ordered: bool,
+    def __init__(self, A: "DeviceCSR", rows: Optional[RowSelection], ordered,
                  task_nnz: int):
         _destroy_retired_plans()
         self.A = A
         self.rows = rows
-        self.ordered = bool(ordered)
+        self.ordered = int(ordered)  # 0 fast, 1 ordered, 2 ordered without column slices
         self.handle = C.c_void_p()
         n_out = rows.n if rows is not None else A.n_rows
         with torch.cuda.device(A.device):
@@ -196,8 +199,11 @@ class Plan:
     def info(self) -> dict:
         a, b, c, d = (C.c_int64() for _ in range(4))
         call("gcg_spmm_plan_info", self.handle, C.byref(a), C.byref(b), C.byref(c), C.byref(d))
+        e, f, g = (C.c_int64() for _ in range(3))
+        call("gcg_spmm_plan_hub_rows", self.handle, C.byref(e), C.byref(f), C.byref(g))
         return {"n_tasks": a.value, "n_long_rows": b.value, "n_segments": c.value,
-                "max_task_nnz": d.value}
+                "max_task_nnz": d.value, "n_coop_rows": e.value, "n_sliced_rows": f.value,
+                "n_slices": g.value}
 
     def workspace(self, K: int) -> Optional[torch.Tensor]:
         nb = C.c_size_t()
@@ -288,9 +294,11 @@ class DeviceCSR:
                                self.indptr.cpu().numpy()), shape=self.shape)
 
     # -- plans & transpose --------------------------------------------------------------
-    def plan(self, rows: Optional[RowSelection] = None, ordered: bool = False,
+    def plan(self, rows: Optional[RowSelection] = None, ordered=False,
              task_nnz: int = 0) -> Plan:
-        key = (rows.key if rows is not None else None, bool(ordered), int(task_nnz))
+        """The launch plan (cached): ordered False / True, or 2 = ordered without column-sliced
+        hub rows (gcg_spmm_plan_create; A/B and tests)."""
+        key = (rows.key if rows is not None else None, int(ordered), int(task_nnz))
         p = self._plans.get(key)
         if p is None:
             p = Plan(self, rows, ordered, task_nnz)
@@ -630,7 +638,8 @@ def spmm(A: DeviceCSR, Z: torch.Tensor, bias: Optional[torch.Tensor] = None,
                  _ptr(A.indices), _ptr(A.data), _ptr(Z), ldz, K, _ptr(out), ldy, _ptr(bias), actc,
                  _ptr(rows_dev), n_out, _ptr(gate), ldg, stream)
         else:
-            plan = A.plan(sel, ordered=(mode == "ordered"), task_nnz=task_nnz)
+            plan = A.plan(sel, ordered=ORDERED_PLAN if mode == "ordered" else 0,
+                          task_nnz=task_nnz)
             ws = plan.workspace(K)
             # the hint is read by the dwordx4 launches only (spmm.hip pick_vec): never built
             # or looked up for a call that gathers narrower vectors

@@ -96,9 +96,13 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
  * reused for every K. Reads indptr (and out_rows) back to the host once and
  * validates indptr; this call synchronizes `stream` -- it is NOT a hot-path call.
  *   task_nnz  : target nonzeros per wave task (0 = default: clamp(nnz / 8192, 32, 512)).
- *   ordered   : 1 = never split a row (bitwise scipy order): rows longer than task_nnz are
- *                   scheduled first, those longer than 8 x task_nnz on a whole workgroup each
- *                   (the storage-order sum handed from wave to wave, still bitwise);
+ *   ordered   : 1 = never split a row's sum (bitwise scipy order): rows longer than task_nnz
+ *                   are scheduled first, those longer than 8 x task_nnz on a whole workgroup
+ *                   each (the storage-order sum handed from wave to wave, still bitwise), cut
+ *                   into 2 column slices on two workgroups when the launch is two 256-float
+ *                   chunks wide (256 < K per 512-float panel, round 5): each slice sums all
+ *                   the row's nonzeros for its columns, in storage order -- still bitwise;
+ *               2 = ordered with every whole-workgroup row unsliced (A/B and tests);
  *               0 = split rows longer than task_nnz into segments (fast).
  */
 typedef struct gcg_spmm_plan gcg_spmm_plan;
@@ -114,6 +118,10 @@ gcg_status gcg_spmm_plan_workspace_bytes(const gcg_spmm_plan* plan, int64_t K, s
  * workgroup in an ordered plan), segments, max task nnz. */
 gcg_status gcg_spmm_plan_info(const gcg_spmm_plan* plan, int64_t* n_tasks, int64_t* n_long_rows,
                               int64_t* n_segments, int64_t* max_task_nnz);
+/* Whole-workgroup rows of an ordered plan: all of them, those cut into column slices, and the
+ * slices per cut row. Ordered plans need no workspace. */
+gcg_status gcg_spmm_plan_hub_rows(const gcg_spmm_plan* plan, int64_t* n_coop_rows,
+                                  int64_t* n_sliced_rows, int64_t* n_slices);
 
 /* Planned SpMM: same contract as gcg_spmm_csr_f32; out_rows/n_out come from the plan. */
 gcg_status gcg_spmm_csr_f32_planned(const gcg_spmm_plan* plan, const int32_t* indptr,
@@ -164,8 +172,9 @@ gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_
 /*
  * Host-only planner (no device memory, no HIP calls): the task list the plan uses,
  * exposed for testing and for host-side tools. `tasks_host` receives n_tasks int32
- * quadruples {a, b, c, d}: d < 0 -> rows of positions [a, b); d >= 0 -> segment of
- * position a covering nonzeros [b, c) into workspace slot d. `long_host` receives
+ * quadruples {a, b, c, d}: c == -4 -> column slice b of d of the row at position a (ordered);
+ * otherwise d < 0 -> rows of positions [a, b) (c == -2: one row on a whole workgroup);
+ * d >= 0 -> segment of position a covering nonzeros [b, c) into workspace slot d. `long_host` receives
  * n_long quadruples {position, first_slot, n_slots, 0}. Pass NULL buffers to size.
  */
 gcg_status gcg_spmm_plan_host(int64_t n_rows, const int32_t* indptr_host,

@@ -70,8 +70,13 @@ def test_planner_covers_every_row_once(native_lib, ordered):
     tasks, longs, nslots = plan_host(indptr, task_nnz=256, ordered=ordered)
     covered = np.zeros(5000, np.int64)
     seg_nnz = np.zeros(5000, np.int64)
+    slices = {}
     for a, b, c, d in tasks:
-        if d < 0:
+        if c == -4:  # column slice b of d of the row at position a (ordered)
+            assert ordered and d == 2
+            slices.setdefault(a, []).append(b)
+            covered[a] += b == 0
+        elif d < 0:
             covered[a:b] += 1
             nnz = indptr[b] - indptr[a]
             assert nnz <= 256 or b - a == 1  # a task over budget is a single (unsplit) row
@@ -83,8 +88,15 @@ def test_planner_covers_every_row_once(native_lib, ordered):
         covered[p] += 1
         assert seg_nnz[p] == lens[p]
     assert np.all(covered == 1)
+    for ks in slices.values():  # both column slices, adjacent
+        assert ks == [0, 1]
     if ordered:
         assert len(longs) == 0 and nslots == 0
+        # every row past 8 x task_nnz is cut into two column slices, longest first, leading
+        sliced = sorted(slices, key=lambda a: -int(lens[a]))
+        assert len(slices) == int((lens > 8 * 256).sum()) > 0
+        first = [t[0] for t in tasks if t[2] == -4][::2]
+        assert first == sliced and all(t[2] == -4 for t in tasks[:2 * len(first)])
     else:
         assert len(longs) == int((lens > 256).sum())
 

@@ -122,3 +122,44 @@ def test_convolution_dense_layer_defaults_to_rectify(cuda, g):
     out = l2.get_output_for(l1.get_output_for(X), target_indices=g["idx"]).detach().cpu().numpy()
     f = O.gcn_forward(X, H, g["W1"], g["b1"], g["W2"], g["b2"], g["idx"])
     assert np.abs(out - O.relu(f["logits"])).max() < 1e-5
+
+
+@pytest.mark.parametrize("with_rows", [True, False])
+def test_reference_order_reassociated_backward(cuda, with_rows, monkeypatch):
+    """ConvolutionDenseLayer in the reference order with C > K (layers._TransformPropagate): the
+    forward is the reference's association (T.dot(h, W2) then S.dot(H, .)), bitwise the autograd
+    composition; the backward re-associated -- dh = H[rows]^T . (g . W2^T), dW2 = (H[rows] .
+    h)^T . g -- within the float64 bars of Theano's association, for a target subset drawn with
+    replacement and for every row."""
+    from graphconvgeo_amd import layers as L
+    n, f, k, c = 30_000, 2_000, 64, 257
+    H = synthetic_graph(n, 250_000)
+    X = synthetic_features(n, f, nnz_per_row=32, empty_frac=0.02)
+    W1, W2 = glorot_uniform(f, k), glorot_uniform(k, c, seed=9)
+    b1 = np.random.default_rng(1).standard_normal(k).astype(np.float32) * 0.01
+    b2 = np.random.default_rng(4).standard_normal(c).astype(np.float32) * 0.01
+    idx = np.random.default_rng(2).choice(20_000, size=20_000).astype(np.int32) if with_rows \
+        else np.arange(n, dtype=np.int32)
+    y = np.random.default_rng(3).integers(0, c, size=idx.size)
+    res = {}
+    for reassoc in (True, False):
+        monkeypatch.setattr(L, "REASSOCIATED_BACKWARD", reassoc)
+        model = GCN(H, X, f, k, c, device=cuda, W1=W1, W2=W2, mode="ordered")
+        assert model.l_out.order == "reference" and model.l_out.num_units > model.l_out.num_inputs
+        with torch.no_grad():
+            model.l_hid1.b.copy_(torch.from_numpy(b1))
+            model.l_out.b.copy_(torch.from_numpy(b2))
+        P = model(idx)
+        loss = torch.nn.functional.nll_loss(torch.log(P), torch.from_numpy(y).to(cuda))
+        loss.backward()
+        torch.cuda.synchronize()
+        res[reassoc] = (P.detach(), [p.grad.clone() for p in (model.l_hid1.W, model.l_out.W,
+                                                                model.l_hid1.b, model.l_out.b)])
+    assert torch.equal(res[True][0], res[False][0])  # the same forward, bitwise
+    fwd = O.gcn_forward(X, H, W1, b1, W2, b2, idx)
+    gr = O.gcn_backward(X, H, W1, W2, fwd, idx, y, regul_coefs=(0.0, 0.0))
+    for reassoc in (True, False):
+        for got, key in zip(res[reassoc][1], ("W1", "W2", "b1", "b2")):
+            ref = gr[key]
+            err = np.abs(got.cpu().numpy() - ref).max()
+            assert err < 1e-5 * max(1.0, np.abs(ref).max()), (reassoc, key, err)

@@ -39,8 +39,12 @@ def test_planner_partitions_work_exactly(native_lib, lens, task_nnz, ordered, us
     covered = np.zeros(n_out, np.int64)
     seg = {}
     slots = set()
+    slices = {}
     for a, b, c, d in tasks:
-        if d < 0:
+        if c == -4:  # column slice b of d of the row at position a (ordered): covered once
+            slices.setdefault(a, []).append(b)
+            covered[a] += b == 0
+        elif d < 0:
             assert 0 <= a < b <= n_out
             covered[a:b] += 1
         else:
@@ -55,6 +59,8 @@ def test_planner_partitions_work_exactly(native_lib, lens, task_nnz, ordered, us
         assert len(parts) == cnt and parts[0][0] == indptr[r] and parts[-1][1] == indptr[r + 1]
         assert all(parts[i][1] == parts[i + 1][0] for i in range(cnt - 1))  # contiguous, in order
     assert np.all(covered == 1)
+    assert all(ks == [0, 1] for ks in slices.values())
+    assert not slices or ordered
     assert slots == set(range(nslots))
     if ordered:
         assert nslots == 0

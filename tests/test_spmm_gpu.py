@@ -486,3 +486,64 @@ def test_ordered_cooperative_world_scale_block(cuda):
     hubs = np.argsort(lens)[-64:]
     sample = np.unique(np.concatenate([hubs, np.random.default_rng(0).choice(n, 2000)]))
     assert np.array_equal(Y[sample], O.spmm_f32(H, Z, rows=sample))
+
+
+@pytest.mark.parametrize("K", [1, 3, 64, 257, 300, 301, 930, 1500, 8200])
+@pytest.mark.parametrize("task_nnz", [32, 128])
+def test_ordered_sliced_hub_rows_bitwise(cuda, K, task_nnz):
+    """'ordered' rows longer than 8 x task_nnz run on whole workgroups; in a launch two 256-float
+    chunks wide each is cut into two column slices on two CUs (spmm.hip coop_slice, round 5),
+    each summing every nonzero of the row for its columns in storage order. Bitwise the oracle:
+    hub rows of every length around the batch, a row subset repeating the hub rows, bias +
+    rectify + gate, padded operands with a masked last vector (K = 257, 930: dwordx4 + tail),
+    unpadded odd widths (K = 301: dword gathers, one slice runs the whole row), several column
+    panels (K = 930, 1500, 8200), repeated launches and HIP-graph replays; ordered plan 2
+    (unsliced) gives the same bits."""
+    lens = [(3, 5000), (20, 12189), (21, 3001), (40, 16 * task_nnz), (41, 16 * task_nnz + 777),
+            (10, 8 * task_nnz + 1), (11, 12 * task_nnz)]
+    n_cols = 30000 if K <= 1500 else 3000
+    H = rand_csr(400, n_cols, 10, seed=K + task_nnz, long_rows=lens, dups=True)
+    Z = np.random.default_rng(K).standard_normal((n_cols, K)).astype(np.float32)
+    b = np.random.default_rng(K + 1).standard_normal(K).astype(np.float32)
+    A = gs.DeviceCSR.from_scipy(H, cuda)
+    info = A.plan(None, True, task_nnz).info()
+    rl = np.diff(H.indptr)
+    n_hub = int((rl > 8 * task_nnz).sum())
+    assert info["n_coop_rows"] == info["n_sliced_rows"] == info["n_long_rows"] == n_hub >= 6
+    assert info["n_slices"] == 2
+    assert A.plan(None, 2, task_nnz).info()["n_sliced_rows"] == 0
+    if K in (257, 930):
+        Zd = gs.empty_dense(n_cols, K, cuda)  # padded rows: dwordx4 with a masked last vector
+        Zd.copy_(to_dev(Z, cuda))
+        assert Zd.stride(0) % 4 == 0 and Zd.stride(0) > K
+    else:
+        Zd = to_dev(Z, cuda)
+    ref = O.spmm_f32(H, Z)
+    Y = gs.spmm(A, Zd, mode="ordered", task_nnz=task_nnz)
+    assert np.array_equal(Y.cpu().numpy(), ref)
+    Y2 = gs.spmm(A, Zd, mode="ordered", task_nnz=task_nnz)
+    assert torch.equal(Y, Y2)
+    try:
+        gs.ORDERED_PLAN = 2
+        assert torch.equal(gs.spmm(A, Zd, mode="ordered", task_nnz=task_nnz), Y)
+    finally:
+        gs.ORDERED_PLAN = 1
+    rows = np.array([20, 3, 3, 7, 41, 40, 20, 0, 11, 21, 10, 20], np.int32)
+    sel = gs.RowSelection(rows, cuda)
+    assert A.plan(sel, True, task_nnz).info()["n_sliced_rows"] == 10
+    gate = gs.empty_gate(rows.size, K, cuda)
+    Yr = gs.spmm(A, Zd, bias=to_dev(b, cuda), act="relu", rows=sel, mode="ordered",
+                 task_nnz=task_nnz, gate=gate).cpu().numpy()
+    pre = O.spmm_f32(H, Z, bias=b, rows=rows)
+    assert np.array_equal(Yr, O.relu(pre))
+    assert np.array_equal(gate.cpu().numpy(), (2 * (pre > 0) + (pre == 0)).astype(np.uint8))
+    if K in (300, 930):  # replayed HIP graph
+        out = gs.empty_dense(400, K, cuda)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            gs.spmm(A, Zd, out=out, mode="ordered", task_nnz=task_nnz)
+        for _ in range(3):
+            out.zero_()
+            g.replay()
+            torch.cuda.synchronize()
+            assert np.array_equal(out.cpu().numpy(), ref)

@@ -46,8 +46,14 @@ def main():
                     help="weight gradients on the main stream (dense.SIDE_STREAM_WEIGHT_GRADS off)")
     ap.add_argument("--inline-head", action="store_true",
                     help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
+    ap.add_argument("--theano-backward", action="store_true",
+                    help="reference order: autograd in Theano's association "
+                         "(layers.REASSOCIATED_BACKWARD off)")
     args = ap.parse_args()
     gs.WIDE_ROW_ALIGN = not args.legacy_stride
+    if args.theano_backward:
+        from graphconvgeo_amd import layers
+        layers.REASSOCIATED_BACKWARD = False
     from graphconvgeo_amd import dense
     if args.nt_math:
         dense.NT_MATH = args.nt_math
@@ -108,6 +114,7 @@ def main():
            "mode": args.mode, "order": args.order, "hip_graph": args.graph,
            "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
            "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
+           "theano_backward": args.theano_backward,
            "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
