@@ -327,17 +327,29 @@ __device__ __forceinline__ void lds_handover_barrier() {
 // A wave issues its next batch's gathers right after its own hand-over, so they fly while the
 // later waves of this batch add. LDS: one row sum (<= 512 floats).
 //
-// coop_sum adds nonzeros [s, e) of one row to the running sum held in sacc (zero at the
-// row's first nonzero), gathering the columns gcol of each Z row: products v * Z[col] rounded,
-// then added (as acc + v * z without FMA).
-template <int VEC, int NCH, int U, int WPB, int HC>
-__device__ __forceinline__ void coop_sum(int s, int e, const int32_t* __restrict__ indices,
+template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
+__device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
+                                         const int32_t* __restrict__ indices,
                                          const float* __restrict__ vals,
+                                         const int32_t* __restrict__ out_rows,
                                          const float* __restrict__ Z, int64_t ldz,
-                                         const int (&gcol)[NCH], float* __restrict__ sacc) {
+                                         const int (&col)[NCH], const int (&gcol)[NCH],
+                                         const bool (&on)[NCH], int K, float* __restrict__ Y,
+                                         int64_t ldy, const float* __restrict__ bias, int act,
+                                         uint8_t* __restrict__ gate, int64_t ldgate,
+                                         float* __restrict__ sacc) {
   const int wave = uniform(static_cast<int>(threadIdx.x >> 6));
   const int lane = threadIdx.x & (kWave - 1);
+  const int r = out_rows ? uniform(out_rows[p]) : p;
+  const int s = uniform(indptr[r]);
+  const int e = uniform(indptr[r + 1]);
   constexpr int B = WPB * U;  // nonzeros per batch
+  if (wave == 0) {
+#pragma unroll
+    for (int k = 0; k < NCH; ++k)
+#pragma unroll
+      for (int q = 0; q < VEC; ++q) sacc[(k * kWave + lane) * VEC + q] = 0.0f;
+  }
   // (col, val) of this wave's nonzeros of a batch: one VECTOR load per wave (lane u holds
   // nonzero u, indices clamped into the row -- coop rows are never empty), prefetched one batch
   // ahead and moved to SGPRs with readlane when the batch is gathered. (Scalar-loaded pairs,
@@ -431,26 +443,7 @@ __device__ __forceinline__ void coop_sum(int s, int e, const int32_t* __restrict
       lds_handover_barrier();
     }
   }
-}
-
-template <int VEC, int NCH>
-__device__ __forceinline__ void sacc_fill(float* __restrict__ sacc, const float* __restrict__ src,
-                                          const int (&gcol)[NCH]) {
-  const int lane = threadIdx.x & (kWave - 1);
-#pragma unroll
-  for (int k = 0; k < NCH; ++k)
-    *reinterpret_cast<Vec<VEC>*>(sacc + (k * kWave + lane) * VEC) =
-        src ? load_vec<VEC>(src + gcol[k]) : Vec<VEC>{};
-}
-
-// bias, gate, rectify and the output row of a whole-workgroup row (wave 0)
-template <int VEC, int NCH, int TL>
-__device__ __forceinline__ void coop_epilogue(int p, const float* __restrict__ sacc,
-                                              const int (&col)[NCH], const bool (&on)[NCH], int K,
-                                              float* __restrict__ Y, int64_t ldy,
-                                              const float* __restrict__ bias, int act,
-                                              uint8_t* __restrict__ gate, int64_t ldgate) {
-  const int lane = threadIdx.x & (kWave - 1);
+  if (wave != 0) return;
   float* yrow = Y + static_cast<int64_t>(p) * ldy;
 #pragma unroll
   for (int k = 0; k < NCH; ++k) {
@@ -468,40 +461,23 @@ __device__ __forceinline__ void coop_epilogue(int p, const float* __restrict__ s
   }
 }
 
-template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
-__device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indptr,
-                                         const int32_t* __restrict__ indices,
-                                         const float* __restrict__ vals,
-                                         const int32_t* __restrict__ out_rows,
-                                         const float* __restrict__ Z, int64_t ldz,
-                                         const int (&col)[NCH], const int (&gcol)[NCH],
-                                         const bool (&on)[NCH], int K, float* __restrict__ Y,
-                                         int64_t ldy, const float* __restrict__ bias, int act,
-                                         uint8_t* __restrict__ gate, int64_t ldgate,
-                                         float* __restrict__ sacc) {
-  const int r = out_rows ? uniform(out_rows[p]) : p;
-  const int s = uniform(indptr[r]);
-  const int e = uniform(indptr[r + 1]);
-  if (uniform(static_cast<int>(threadIdx.x >> 6)) == 0) sacc_fill<VEC, NCH>(sacc, nullptr, gcol);
-  coop_sum<VEC, NCH, U, WPB, HC>(s, e, indices, vals, Z, ldz, gcol, sacc);
-  if (uniform(static_cast<int>(threadIdx.x >> 6)) != 0) return;
-  coop_epilogue<VEC, NCH, TL>(p, sacc, col, on, K, Y, ldy, bias, act, gate, ldgate);
-}
-
 // Column-sliced hub rows (round 5). One CU's ordered sum of a hub row is bound by the rows it
 // has in flight (~19 GB/s for 1216-B random rows: 0.66 ms for a 12k-nonzero row of a P = 8
 // World block, longer than the rest of that block's launch). The columns are independent, so
 // a row of a two-chunk launch (NCH = 2) is cut into two column slices, each a whole-workgroup
 // task on its own CU that runs coop_sum over ALL the row's nonzeros for its half of the
 // columns: every column's additions are the single-wave loop's, in storage order (bitwise).
-// Half the floats per gathered row let a wave keep twice the rows in flight (U x NCH rows of
-// one chunk in the same registers), so each slice streams its row in half the time. (A
-// chained design -- row chunks on several CUs handing the running sum over through a flag
-// -- was built and measured first: 1.66 ms for the P = 8 block vs 1.04 whole-row, its phase
-// that adds stored products being as latency-bound as the gather)
-// Task {position, slice, -4, slices}. Launches of one chunk (NCH = 1: K <= 256 at dwordx4)
-// gain nothing from a slice, and the wider-chunk dword / dwordx2 launches (rows whose stride is
-// not a multiple of 4 floats) are not cut: slice 0 runs the whole row (coop_row), others exit.
+// Half the floats per gathered row let a wave keep twice the rows in flight (coop_row over one
+// chunk with 2U rows per batch, the same registers), so each slice streams its row in ~0.6
+// the time. (A chained design -- row chunks on several CUs handing the running sum over
+// through a flag -- was built and measured first: 1.66 ms for the P = 8 block vs 1.04
+// whole-row, its phase that adds stored products being as latency-bound as the gather;
+// DESIGN.md §1.1.) Task {position, slice, -4, slices}. Launches of one chunk (NCH = 1: K <= 256
+// at dwordx4) gain nothing from a slice, and the wider-chunk dword / dwordx2 launches (rows
+// whose stride is not a multiple of 4 floats) are not cut: slice 0 runs the whole row, the
+// others exit. Compiled only into the SLC = 1 kernels, which run plans with cut rows: inlined
+// beside the bulk path, its deeper batch changes that path's register allocation (the K = 300
+// kernel's row tasks: X.W1 on Twitter-US 1.71 -> 2.08 ms with no cut row in the launch).
 template <int VEC, int NCH, int U, int WPB, int HC = 0, int TL = 0>
 __device__ __forceinline__ void coop_slice(int p, int sl, int n_sl,
                                            const int32_t* __restrict__ indptr,
@@ -519,10 +495,10 @@ __device__ __forceinline__ void coop_slice(int p, int sl, int n_sl,
       coop_row<VEC, NCH, U, WPB, HC, TL>(p, indptr, indices, vals, out_rows, Z, ldz, col, gcol,
                                          on, K, Y, ldy, bias, act, gate, ldgate, sacc);
   } else {
-    constexpr int US = U * NCH > kWave ? kWave : U * NCH;  // rows in flight per wave
+    constexpr int US = 2 * U > kWave ? kWave : 2 * U;  // rows in flight per wave: one chunk
     const int lane = threadIdx.x & (kWave - 1);
     const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);
-    const int wp = min(kWave * VEC * NCH, K - panel0);                // panel width (floats)
+    const int wp = min(kWave * VEC * NCH, K - panel0);  // panel width (floats)
     const int ws = min(kWave * VEC, ((wp + n_sl - 1) / n_sl + VEC - 1) / VEC * VEC);
     const int c0 = panel0 + sl * ws;
     const int c1 = min(c0 + ws, panel0 + wp);
@@ -532,14 +508,8 @@ __device__ __forceinline__ void coop_slice(int p, int sl, int n_sl,
     scol[0] = c0 + lane * VEC;
     son[0] = scol[0] < c1;
     sgcol[0] = son[0] ? scol[0] : c0;
-    const int r = out_rows ? uniform(out_rows[p]) : p;
-    const int s = uniform(indptr[r]);
-    const int e = uniform(indptr[r + 1]);
-    const int wave = uniform(static_cast<int>(threadIdx.x >> 6));
-    if (wave == 0) sacc_fill<VEC, 1>(sacc, nullptr, sgcol);
-    coop_sum<VEC, 1, US, WPB, HC>(s, e, indices, vals, Z, ldz, sgcol, sacc);
-    if (wave != 0) return;
-    coop_epilogue<VEC, 1, TL>(p, sacc, scol, son, K, Y, ldy, bias, act, gate, ldgate);
+    coop_row<VEC, 1, US, WPB, HC, TL>(p, indptr, indices, vals, out_rows, Z, ldz, scol, sgcol,
+                                      son, K, Y, ldy, bias, act, gate, ldgate, sacc);
   }
 }
 
@@ -549,10 +519,9 @@ __device__ __forceinline__ void coop_slice(int p, int sl, int n_sl,
 //   task.w >= 0      : position task.x, nonzeros [task.y, task.z) -> workspace slot task.w
 // The first n_coop tasks ('ordered' long rows, longest first) take a whole workgroup each
 // (coop_row); the other tasks one wave each, in the blocks after them.
-template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0, int TL = 0>
-// waves_per_eu(3): the K = 300 variant (VEC 4 x NCH 2, U = 16) otherwise lands one VGPR past
-// three waves per SIMD (169) once coop_slice's deeper batch is inlined beside the bulk path.
-__global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(3))) void spmm_rows_kernel(
+template <int VEC, int NCH, int U, int WPB = kWavesPerBlock, int SUB = 1, int HC = 0, int TL = 0,
+          int SLC = 0>
+__global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     const int4* __restrict__ tasks, int n_tasks, int n_coop, int n_out,
     const int32_t* __restrict__ indptr,
     const int32_t* __restrict__ indices, const float* __restrict__ vals,
@@ -575,15 +544,18 @@ __global__ __launch_bounds__(kWave * WPB) __attribute__((amdgpu_waves_per_eu(3))
   }
   if (blk < n_coop) {  // a whole-workgroup long row or slice of one (uniform across the block)
     __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
-    const int4 t0 = tasks[blk];
-    if (uniform(t0.z) == -4) {  // {position, slice, -4, slices}
-      coop_slice<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), uniform(t0.y), uniform(t0.w), indptr,
-                                           indices, vals, out_rows, Z, ldz, col, gcol, on, K, Y,
-                                           ldy, bias, act, gate, ldgate, sacc);
-    } else {
-      coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), indptr, indices, vals, out_rows, Z, ldz,
-                                         col, gcol, on, K, Y, ldy, bias, act, gate, ldgate, sacc);
+    if constexpr (SLC) {
+      const int4 t0 = tasks[blk];
+      if (uniform(t0.z) == -4) {  // {position, slice, -4, slices}
+        coop_slice<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), uniform(t0.y), uniform(t0.w), indptr,
+                                             indices, vals, out_rows, Z, ldz, col, gcol, on, K, Y,
+                                             ldy, bias, act, gate, ldgate, sacc);
+        return;
+      }
     }
+    coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z,
+                                       ldz, col, gcol, on, K, Y, ldy, bias, act, gate, ldgate,
+                                       sacc);
     return;
   }
   const int w = uniform(n_coop + (blk - n_coop) * WPB + (threadIdx.x >> 6));
@@ -741,6 +713,8 @@ struct LaunchArgs {
   const int32_t* hint = nullptr;
   // K % VEC != 0 on VEC-padded rows: the last vector of a row is masked (TL = 1 kernels)
   int tail = 0;
+  // the plan cuts rows into column slices (coop_slice): the SLC = 1 kernels
+  int sliced = 0;
 };
 
 template <int VEC, int NCH, int U, int WPB, int SUB = 1, int HC = 0>
@@ -748,6 +722,21 @@ void launch_rows_u(const LaunchArgs& a, int n_panels, hipStream_t stream) {
   // plan-less: one wave per SUB consecutive rows
   const int n_tasks = a.tasks == nullptr ? (a.n_tasks + SUB - 1) / SUB : a.n_tasks;
   const dim3 grid(a.n_coop + (n_tasks - a.n_coop + WPB - 1) / WPB, n_panels);
+  if constexpr (VEC == 4 && NCH == 2 && SUB == 1) {  // column-sliced hub rows
+    if (a.sliced) {
+      if (a.tail)
+        hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 1, 1>), grid,
+                           dim3(kWave * WPB), 0, stream, a.tasks, n_tasks, a.n_coop, a.n_tasks,
+                           a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y, a.ldy,
+                           a.bias, a.act, a.ws, a.ldws, a.gate, a.ldgate);
+      else
+        hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 0, 1>), grid,
+                           dim3(kWave * WPB), 0, stream, a.tasks, n_tasks, a.n_coop, a.n_tasks,
+                           a.indptr, a.indices, a.vals, a.out_rows, a.Z, a.ldz, a.K, a.Y, a.ldy,
+                           a.bias, a.act, a.ws, a.ldws, a.gate, a.ldgate);
+      return;
+    }
+  }
   if constexpr (VEC == 4) {
     if (a.tail) {
       hipLaunchKernelGGL((spmm_rows_kernel<VEC, NCH, U, WPB, SUB, HC, 1>), grid, dim3(kWave * WPB),
@@ -903,8 +892,15 @@ struct HostPlan {
   int64_t n_sliced = 0;      // ... of which cut into column slices (coop_slice)
 };
 
-// Column slices per whole-workgroup row (ordered == 1; ordered == 2 keeps whole rows)
+// Column slices per cut row. A whole-workgroup row is cut (ordered == 1; ordered == 2 keeps
+// every row whole) when it is also longer than 1/kSliceDivisor of the plan's nonzeros: where
+// one CU's sum of it would outlast the rest of the launch (~55 ns per 1216-B row on one CU vs
+// ~5.8 G rows/s for the bulk: rows past ~1/320 of the work). Cutting every whole-workgroup row
+// costs throughput -- two half rows fetch ~10 % more lines than one, twice the per-row issue
+// -- and a launch of many of them (X^T.g's Zipf-tail features on Twitter-US) ran 1.69 -> 1.98
+// ms. World P = 8 blocks cut their ~12k-nonzero hub rows; the whole graph cuts none.
 constexpr int kHubSlices = 2;
+constexpr int64_t kSliceDivisor = 768;
 
 // 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
 // long rows stay single-wave tasks scheduled first: 8 x task_nnz (4096 at Twitter-World). Measured (World power-law,
@@ -991,10 +987,10 @@ gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t*
   std::stable_sort(long_rows.begin(), long_rows.end(), longest_first);
   std::vector<int32_t> head;
   head.reserve((coop_rows.size() * kHubSlices + long_rows.size()) * 4 + seg_tasks.size());
-  // whole-workgroup rows first, longest first: the column slices of every row (ordered == 1),
-  // or the whole row on one workgroup (ordered == 2: A/B and tests)
+  // whole-workgroup rows first, longest first: cut into column slices or whole
+  const int64_t slice_min = std::max(coop_min, work / kSliceDivisor);
   for (const auto& lr : coop_rows) {
-    if (ordered == 1) {
+    if (ordered == 1 && lr.first >= slice_min) {
       for (int k = 0; k < kHubSlices; ++k)
         head.insert(head.end(), {int32_t(lr.second), k, -4, kHubSlices});
       ++hp->n_sliced;
@@ -1227,6 +1223,7 @@ gcg_status gcg_spmm_csr_f32_planned_hint(const gcg_spmm_plan* plan, const int32_
   LaunchArgs a{plan->tasks, plan->n_tasks, indptr, indices, vals, plan->out_rows, Z, ldz, int(K),
                Y, ldy, bias, act, ws, ldws, plan->task_nnz, gate, ldgate, plan->n_coop,
                gather_hint};
+  a.sliced = plan->n_sliced > 0 ? 1 : 0;
   const int vec = pick_vec(Z, ldz, Y, ldy, K, bias, ws, ldws, &a.tail);
   if (gcg_status s = launch_spmm(a, vec, st)) return s;
   if (plan->n_long > 0) {

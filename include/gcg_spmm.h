@@ -98,10 +98,11 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
  *   task_nnz  : target nonzeros per wave task (0 = default: clamp(nnz / 8192, 32, 512)).
  *   ordered   : 1 = never split a row's sum (bitwise scipy order): rows longer than task_nnz
  *                   are scheduled first, those longer than 8 x task_nnz on a whole workgroup
- *                   each (the storage-order sum handed from wave to wave, still bitwise), cut
- *                   into 2 column slices on two workgroups when the launch is two 256-float
- *                   chunks wide (256 < K per 512-float panel, round 5): each slice sums all
- *                   the row's nonzeros for its columns, in storage order -- still bitwise;
+ *                   each (the storage-order sum handed from wave to wave, still bitwise); one
+ *                   also longer than 1/768 of the plan's nonzeros is cut into 2 column slices
+ *                   on two workgroups when the launch is two 256-float chunks wide (256 < K
+ *                   per 512-float panel, round 5): each slice sums all the row's nonzeros for
+ *                   its columns, in storage order -- still bitwise;
  *               2 = ordered with every whole-workgroup row unsliced (A/B and tests);
  *               0 = split rows longer than task_nnz into segments (fast).
  */

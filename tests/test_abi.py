@@ -92,9 +92,10 @@ def test_planner_covers_every_row_once(native_lib, ordered):
         assert ks == [0, 1]
     if ordered:
         assert len(longs) == 0 and nslots == 0
-        # every row past 8 x task_nnz is cut into two column slices, longest first, leading
+        # rows past 8 x task_nnz and 1/768 of the work: two column slices, longest first, leading
         sliced = sorted(slices, key=lambda a: -int(lens[a]))
-        assert len(slices) == int((lens > 8 * 256).sum()) > 0
+        slice_min = max(8 * 256, int(lens.sum()) // 768)
+        assert len(slices) == int(((lens > 8 * 256) & (lens >= slice_min)).sum()) > 0
         first = [t[0] for t in tasks if t[2] == -4][::2]
         assert first == sliced and all(t[2] == -4 for t in tasks[:2 * len(first)])
     else:

@@ -492,7 +492,8 @@ def test_ordered_cooperative_world_scale_block(cuda):
 @pytest.mark.parametrize("task_nnz", [32, 128])
 def test_ordered_sliced_hub_rows_bitwise(cuda, K, task_nnz):
     """'ordered' rows longer than 8 x task_nnz run on whole workgroups; in a launch two 256-float
-    chunks wide each is cut into two column slices on two CUs (spmm.hip coop_slice, round 5),
+    chunks wide those also past 1/768 of the plan's nonzeros (here: all) are cut into two column
+    slices on two CUs (spmm.hip coop_slice, round 5),
     each summing every nonzero of the row for its columns in storage order. Bitwise the oracle:
     hub rows of every length around the batch, a row subset repeating the hub rows, bias +
     rectify + gate, padded operands with a masked last vector (K = 257, 930: dwordx4 + tail),
@@ -509,6 +510,7 @@ def test_ordered_sliced_hub_rows_bitwise(cuda, K, task_nnz):
     info = A.plan(None, True, task_nnz).info()
     rl = np.diff(H.indptr)
     n_hub = int((rl > 8 * task_nnz).sum())
+    assert rl[rl > 8 * task_nnz].min() * 768 >= H.nnz  # every hub row past 1/768 of the work
     assert info["n_coop_rows"] == info["n_sliced_rows"] == info["n_long_rows"] == n_hub >= 6
     assert info["n_slices"] == 2
     assert A.plan(None, 2, task_nnz).info()["n_sliced_rows"] == 0

@@ -2,7 +2,8 @@
 """The row-partitioned local SpMM per mode: for P = 2, 4, 8, every
 rank's block of the World power-law graph (K = 300, all-gathered operand layout) timed in
 'ordered' (bitwise scipy), 'fast' (split hub rows) and 'rowwise'; the slowest rank bounds the
-step. One GPU plays every rank in turn. HIP events, mean of 10 after 3 warm-ups."""
+step. One GPU plays every rank in turn. HIP events, mean of 10 after 3 warm-ups. A mode
+'ordered:256' runs the plan with that task size (whole-workgroup rows past 8 x of it)."""
 import os
 import sys
 
@@ -41,7 +42,8 @@ for P in [int(x) for x in os.environ.get("PARTS", "1,2,4,8").split(",")]:
         Y = gs.empty_dense(part.n_local, K, dev)
         line = []
         for mode in os.environ.get("MODES", "ordered,fast,rowwise").split(","):
-            ms = timed(lambda: gs.spmm(part.A, operand, out=Y, mode=mode))
+            m, _, tn = mode.partition(":")  # "ordered:256": the plan's task size
+            ms = timed(lambda: gs.spmm(part.A, operand, out=Y, mode=m, task_nnz=int(tn or 0)))
             worst[mode] = max(worst.get(mode, 0.0), ms)
             line.append(f"{mode} {ms:.3f}")
         print(f"{kind} P={P} rank={r} nnz={part.nnz_local} longest={part.A.max_row_nnz()} "
