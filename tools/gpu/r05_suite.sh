@@ -1,9 +1,9 @@
 #!/bin/bash
 # Round 5: the whole -m gpu suite (every failure listed), smoke(), then the default bench line
-# with the live kernel-trace stats kept under gpurun_out/r05/prof.
+# with the live kernel-trace stats kept under gpurun_out/r05f/prof.
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
-out=gpurun_out/r05
+out=gpurun_out/r05f
 mkdir -p $out/prof
 timeout -k 10 1000 python -u -m pytest -q --tb=short --maxfail=25 --timeout 600 --timeout-method thread -m gpu tests > $out/tests.log 2>&1
 rc=$?
