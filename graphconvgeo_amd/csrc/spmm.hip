@@ -903,7 +903,7 @@ constexpr int kHubSlices = 2;
 constexpr int64_t kSliceDivisor = 768;
 
 // 'ordered' rows longer than this many nonzeros run on a whole workgroup (coop_row); shorter
-// long rows stay single-wave tasks scheduled first: 8 x task_nnz (4096 at Twitter-World). Measured (World power-law,
+// long rows stay single-wave tasks scheduled first: 8 x task_nnz (1024 with the ordered default task of 128). Measured (World power-law,
 // K = 300, slowest of P row blocks, tools/exp_block_modes.py): P = 4 2.12 -> 1.70 ms, P = 8
 // 1.59 -> 1.16 ms, P = 1 and 2 unchanged; thresholds 1024 / 2048 / 4096 within noise of each
 // other. One hub row alone is bound by its CU (~19 GB/s per CU for 1216-B random rows: 0.77 ms
@@ -912,15 +912,23 @@ constexpr int64_t kSliceDivisor = 768;
 int64_t coop_min_nnz(int64_t task_nnz) { return 8 * task_nnz; }
 
 // Default task size: 512 nonzeros, smaller on small graphs so the launch still has
-// >= ~8k waves (256 CUs x 32 waves) to spread; never below 32.
-int64_t default_task_nnz(int64_t nnz) {
-  int64_t w = nnz / 8192;
-  return w < 32 ? 32 : (w > kDefaultTaskNnz ? kDefaultTaskNnz : w);
+// >= ~8k waves (256 CUs x 32 waves) to spread; never below 32. Ordered plans (round 5): 128,
+// from 32k nonzeros per 1/32768 of the work -- four times the tasks, whole-workgroup rows from
+// 1,024 nonzeros, and the U = 8 batch (5 waves per SIMD) of the < 256-nonzero tasks. World
+// power-law K = 300, slowest of P row blocks (tools/exp_block_modes.py, one box, ordered at
+// 512 / 256 / 128 / 64): P = 1 6.344 / 6.313 / 6.285 / 6.376 ms, P = 4 1.666 / 1.634 / 1.620 /
+// 1.636, P = 8 0.919 / 0.854 / 0.822 / 0.821 (`fast` 7.238 / 1.824 / 0.942 on that box): the
+// rows of 512..4096 nonzeros no longer run on one wave (up to ~0.5 ms each).
+constexpr int64_t kDefaultOrderedTaskNnz = 128;
+int64_t default_task_nnz(int64_t nnz, int ordered) {
+  const int64_t cap = ordered ? kDefaultOrderedTaskNnz : kDefaultTaskNnz;
+  int64_t w = nnz / (ordered ? 32768 : 8192);
+  return w < 32 ? 32 : (w > cap ? cap : w);
 }
 
 gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t* out_rows,
                            int64_t n_out, int64_t task_nnz, int ordered, HostPlan* hp) {
-  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows]);
+  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows], ordered);
   if (indptr[0] != 0) return fail(GCG_ERR_BAD_CSR, "indptr[0] = %d != 0", indptr[0]);
   for (int64_t r = 0; r < n_rows; ++r)
     if (indptr[r + 1] < indptr[r]) return fail(GCG_ERR_BAD_CSR, "indptr decreases at row %lld", (long long)r);
@@ -1117,7 +1125,7 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
   gcg_spmm_plan* p = new (std::nothrow) gcg_spmm_plan();
   if (p == nullptr) return fail(GCG_ERR_ALLOC, "plan allocation failed");
   p->n_rows = n_rows; p->n_cols = n_cols; p->nnz = nnz; p->n_out = n_out;
-  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz);
+  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz, ordered);
   p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
   p->n_long = static_cast<int>(hp.longs.size() / 4);
   p->n_coop = static_cast<int>(hp.n_coop);

@@ -353,11 +353,14 @@ class ConvolutionDenseLayer(GraphConvLayer):
         sparse_in = isinstance(input, gs.DeviceCSR) or sps.issparse(input)
         if (self.order == "reference" and not sparse_in and REASSOCIATED_BACKWARD
                 and self.fused_act is None and self.num_units > self.num_inputs
-                and torch.is_grad_enabled() and not torch.compiler.is_compiling()):
+                and torch.is_grad_enabled()):
             rows = None
             if target_indices is not None:
                 rows = target_indices if isinstance(target_indices, gs.RowSelection) else \
                     gs.RowSelection(target_indices, self.device)
+            if torch.compiler.is_compiling():  # the registered twin (graphconvgeo_amd.ops)
+                Y = _ops.transform_propagate(input, self.W, self.b, self.H, rows, self.mode)
+                return self.post(Y) if self.post is not None else Y
             proj = dense.projection_of(self.W)
             Wa, slot = dense._weight_on_side_stream(self.W)
             Y = _TransformPropagate.apply(input, Wa, self.b, self.H, rows, self.mode, slot, proj)

@@ -267,6 +267,55 @@ def _px_backward(ctx, g_loss, _g_acc, _g_G):
 project_softmax_xent_op.register_autograd(_px_backward, setup_context=_px_setup)
 
 
+# -- gcg::transform_propagate (the reference order's output layer, re-associated backward) ------
+@torch.library.custom_op(f"{LIB}::transform_propagate", mutates_args=())
+def transform_propagate_op(h: Tensor, W: Tensor, b: Optional[Tensor], csr: int, rows: int,
+                           mode: str) -> Tensor:
+    """(S.dot(H, T.dot(h, W)) + b)[rows] (mlpconv.py:88-94) as the reference associates it:
+    the NT GEMM, then the C-wide SpMM. The compiled twin of layers._TransformPropagate."""
+    from . import dense
+    Z = dense.gemm_nt(h, _padded(W, True))
+    return gs.spmm(gs.registered(csr), Z, bias=b, rows=_rows_arg(rows), mode=mode)
+
+
+@transform_propagate_op.register_fake
+def _(h, W, b, csr, rows, mode):
+    return _dense_like(_n_out(csr, rows), W.shape[1], h.device)
+
+
+def _tp_setup(ctx, inputs, output):
+    h, W, b, csr, rows, mode = inputs
+    ctx.csr, ctx.rows, ctx.mode = csr, rows, mode
+    ctx.has_b = b is not None
+    ctx.save_for_backward(h, W)
+
+
+def _tp_backward(ctx, g):
+    """dh = H[rows]^T . (g . W^T), dW = (H[rows] . h)^T . g, db = colsum(g): the re-associated
+    backward of layers._TransformPropagate, from the other ops (the same kernels, bitwise)."""
+    h, W = ctx.saved_tensors
+    gh = gW = gb = None
+    if ctx.has_b and ctx.needs_input_grad[2]:
+        gb = torch.ops.gcg.column_sum(g)
+    if ctx.needs_input_grad[1]:
+        P, _ = torch.ops.gcg.spmm_csr(h, None, ctx.csr, ctx.rows, "none", ctx.mode, False)
+        gW = torch.ops.gcg.gemm_tn(P, g, None)
+    if ctx.needs_input_grad[0]:
+        GW = torch.ops.gcg.gemm_nt(g, _padded(W, False), None, "none")
+        gh, _ = torch.ops.gcg.spmm_csr_backward(GW, g.new_empty(0, dtype=torch.uint8), ctx.csr,
+                                                ctx.rows, ctx.mode, False, True, False)
+    return gh, gW, gb, None, None, None
+
+
+transform_propagate_op.register_autograd(_tp_backward, setup_context=_tp_setup)
+
+
+def transform_propagate(h: Tensor, W: Tensor, b: Optional[Tensor], A, rows=None,
+                        mode: str = "auto") -> Tensor:
+    return torch.ops.gcg.transform_propagate(h, W, b, A.op_id,
+                                             -1 if rows is None else rows.op_id, mode)
+
+
 def dense_matmul(A: Tensor, W: Tensor, b: Optional[Tensor] = None) -> Tensor:
     return torch.ops.gcg.dense_matmul(A, W, b)
 

@@ -22,7 +22,7 @@ class _Rows:  # stand-in for a RowSelection
 
 def test_every_op_is_registered():
     for name in ("spmm_csr", "spmm_csr_backward", "gemm_nt", "gemm_tn", "column_sum",
-                 "dense_matmul", "project_softmax_xent"):
+                 "dense_matmul", "project_softmax_xent", "transform_propagate"):
         assert hasattr(torch.ops.gcg, name), name
 
 
@@ -55,6 +55,19 @@ def test_dense_fakes():
         assert loss.shape == () and acc.shape == () and G.shape == (37, 930)
         assert torch.ops.gcg.gemm_tn(P, C, None).shape == (300, 930)
         assert torch.ops.gcg.column_sum(C).shape == (930,)
+
+
+def test_transform_propagate_fake():
+    """gcg::transform_propagate, the reference order's output layer: [rows of H] x C."""
+    A, R = _Operator(1000, 1000), _Rows(37)
+    with FakeTensorMode():
+        h = torch.empty((1000, 32), device="cuda")
+        W = torch.empty((32, 930), device="cuda")
+        b = torch.empty(930, device="cuda")
+        Y = torch.ops.gcg.transform_propagate(h, W, b, A.op_id, R.op_id, "ordered")
+        assert Y.shape == (37, 930) and Y.stride() == (gs.row_stride(930), 1)
+        Y = torch.ops.gcg.transform_propagate(h, W, None, A.op_id, -1, "ordered")
+        assert Y.shape == (1000, 930)
 
 
 def test_unknown_operator_id_raises():

@@ -51,15 +51,11 @@ def test_opcheck_dense(cuda):
 
 
 @pytest.mark.parametrize("order", ["reference", "propagate_first"])
-def test_compiled_gcn_forward_backward_bitwise_eager(cuda, order, monkeypatch):
-    """The compiled graph differentiates through the registered ops, i.e. in Theano's
-    association; eager runs the reference order's re-associated backward when C > K
-    (layers._TransformPropagate, checked against float64 in test_layers_gpu.py), so the
-    bitwise comparison turns it off for the eager side."""
+def test_compiled_gcn_forward_backward_bitwise_eager(cuda, order):
+    """Reference order with C > K (here 40 > 32): eager runs layers._TransformPropagate (the
+    re-associated backward) and the compiled graph its registered twin gcg::transform_propagate,
+    built from the same kernels -- bitwise equal, forward and every gradient."""
     import torch._dynamo as dynamo
-    from graphconvgeo_amd import layers
-
-    monkeypatch.setattr(layers, "REASSOCIATED_BACKWARD", False)
 
     H, X, idx, W1, W2 = _problem()
     model = GCN(H, X, 200, 32, 40, device=cuda, W1=W1, W2=W2, mode="ordered")

@@ -35,7 +35,12 @@ def test_planner_partitions_work_exactly(native_lib, lens, task_nnz, ordered, us
         rows = np.array(data.draw(st.lists(st.integers(0, n - 1), min_size=0, max_size=300)), np.int32)
     n_out = n if rows is None else len(rows)
     tasks, longs, nslots = _plan(indptr, task_nnz, int(ordered), rows)
-    W = task_nnz if task_nnz > 0 else max(32, min(512, int(indptr[-1]) // 8192))
+    if task_nnz > 0:
+        W = task_nnz
+    elif ordered:  # spmm.hip default_task_nnz: 128 for ordered plans (round 5)
+        W = max(32, min(128, int(indptr[-1]) // 32768))
+    else:
+        W = max(32, min(512, int(indptr[-1]) // 8192))
     covered = np.zeros(n_out, np.int64)
     seg = {}
     slots = set()
