@@ -1194,12 +1194,13 @@ struct Nt3rCfg {
   static constexpr int OCC = OCC_LDS < 1 ? 1 : (OCC_LDS > OCC_REG ? OCC_REG : OCC_LDS);
 };
 
-template <int RT, int G, int WR, int WC>
+template <int RT, int G, int WR, int WC, int V = 0>
 __global__ __launch_bounds__(64 * WR * WC, (Nt3rCfg<RT, G, WR, WC>::OCC)) void
 gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                  const unsigned* __restrict__ Bs, const float* __restrict__ Bt, int64_t ldbt, const float* __restrict__ bias, int act,
                  float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
   using Cfg = Nt3rCfg<RT, G, WR, WC>;
+  constexpr bool PL = (V & 1) != 0;
   constexpr int EPI = 0;
   const int32_t* labels = nullptr;
   float scale = 0.f;
@@ -1305,6 +1306,19 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       load_a(c + 1, nlo, nhi);
     }
     const int kc0 = c * 32;
+    const float* bsec = smem + (c & 1) * STAGE;
+    // PL = 1: the weight planes of slot (g, e) + 1 are read from LDS before slot (g, e)'s
+    // MFMAs are issued (the scheduler is fenced at each slot), so a read's latency hides behind
+    // RT x 6 MFMAs instead of being waited on right before its own
+    auto rd_planes = [&](int ge, bf8 (&bb)[3]) {
+      const int rb = brow0 + 64 * (ge >> 2) + 16 * (ge & 3);
+      const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        bb[p] = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + p * Cfg::P_FLOATS + so));
+    };
+    bf8 bq[2][3];
+    if constexpr (PL) rd_planes(0, bq[0]);
     bf8 ap[RT][3];
 #pragma unroll
     for (int t = 0; t < RT; ++t) {
@@ -1319,7 +1333,26 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       }
       split3(x, ap[t][0], ap[t][1], ap[t][2]);
     }
-    const float* bsec = smem + (c & 1) * STAGE;
+    if constexpr (PL) {
+#pragma unroll
+      for (int ge = 0; ge < 4 * G; ++ge) {
+        if (ge + 1 < 4 * G) rd_planes(ge + 1, bq[(ge + 1) & 1]);
+        __builtin_amdgcn_sched_barrier(0);
+        const int g = ge >> 2, e = ge & 3;
+        const bf8 (&bb)[3] = bq[ge & 1];
+#pragma unroll
+        for (int t = 0; t < RT; ++t) {  // smallest planes first
+          f4 cc = acc[t][g][e];
+          cc = mfma_bf(ap[t][2], bb[0], cc);
+          cc = mfma_bf(ap[t][1], bb[1], cc);
+          cc = mfma_bf(ap[t][0], bb[2], cc);
+          cc = mfma_bf(ap[t][1], bb[0], cc);
+          cc = mfma_bf(ap[t][0], bb[1], cc);
+          acc[t][g][e] = mfma_bf(ap[t][0], bb[0], cc);
+        }
+      }
+      return;
+    }
 #pragma unroll
     for (int g = 0; g < G; ++g)
 #pragma unroll
@@ -2265,12 +2298,12 @@ gcg_status launch_nt3_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   return GCG_OK;
 }
 
-template <int RT, int G, int WR, int WC>
+template <int RT, int G, int WR, int WC, int V = 0>
 gcg_status launch_nt3r_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
-  hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC>), dim3(static_cast<unsigned>(rt * ct)),
+  hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC, V>), dim3(static_cast<unsigned>(rt * ct)),
                      dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
                      a.act, a.C, a.ldc, static_cast<int>(ct));
   GCG_HIP_CHECK(hipGetLastError());
@@ -2342,6 +2375,7 @@ constexpr Nt3Shape kNt3Tiles[] = {
     {2, 2, 4, 1, 2},  // 6: LDS A, 128 x 128
     {2, 1, 4, 2, 2},  // 7: LDS A, 2 column waves
     {4, 1, 4, 1, 2},  // 8: LDS A, 256 x 64
+    {2, 3, 4, 1, 1},  // 9: register A, 128 x 192, weight planes read one slot ahead (PL)
 };
 constexpr int kNt3TileCount = sizeof(kNt3Tiles) / sizeof(kNt3Tiles[0]);
 
@@ -2354,7 +2388,11 @@ Nt3Shape pick_nt3_shape(int64_t N, int64_t K) {
   int best = 1;
   for (int g = 1; g <= 3; ++g)
     if (pad[g] == least || (K > 512 && 4 * pad[g] <= 5 * least)) best = g;
-  return Nt3Shape{2, best, 4, 1, 0};
+  // G = 3 reads the weight planes one slot ahead (PL, bitwise the same products in the same
+  // order): 840k x 930 x 300 172.5-173.0 -> 176.1-176.8, 840k x 300 x 930 176.0-176.8 vs
+  // 174.9-177.1 (profiles/r05/nt_planes_ahead.jsonl); at G = 1 / 2 the fenced schedule lost
+  // (164 / 153 vs 169 / 172), so they keep the compiler's
+  return Nt3Shape{2, best, 4, 1, best == 3 ? 1 : 0};
 }
 gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const unsigned* Bs) {
 #define GCG_NT3_CASE(rt_, g_, wr_, wc_, s_)                                                    \
@@ -2373,6 +2411,8 @@ gcg_status launch_nt3(const Nt3Shape& sh, hipStream_t st, const NtArgs& a, const
   GCG_NT3R_CASE(2, 3, 4, 1)
   GCG_NT3R_CASE(4, 1, 4, 1)
 #undef GCG_NT3R_CASE
+  if (sh.RT == 2 && sh.G == 3 && sh.WR == 4 && sh.WC == 1 && sh.S == 1)  // planes one slot ahead
+    return launch_nt3r_t<2, 3, 4, 1, 1>(a, Bs, st);
   return fail(GCG_ERR_INVALID_ARG, "gemm_nt bf16x6: no tile RT=%d G=%d WR=%d WC=%d S=%d",
               sh.RT, sh.G, sh.WR, sh.WC, sh.S);
 }

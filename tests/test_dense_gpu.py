@@ -423,17 +423,17 @@ def test_gemm_nt_tile_variants(cuda, tile):
 @pytest.mark.parametrize("M,K,N", [(333, 301, 133), (1000, 300, 930), (517, 930, 300),
                                    (70, 33, 65), (1, 5, 3)])
 def test_gemm_nt_bf16x6_tiles_bitwise(cuda, M, K, N):
-    """Every bf16x6 tile (gcg_gemm_nt math GCG_MATH_BF16X6, tiles 0..8: A in registers or through
-    LDS) and the in-loop split of both operands accumulate the same six plane products in the
+    """Every bf16x6 tile (gcg_gemm_nt math GCG_MATH_BF16X6, tiles 0..9: A in registers or through
+    LDS, the weight planes read from LDS one slot ahead or not) and the in-loop split of both operands accumulate the same six plane products in the
     same order: bitwise equal to each other, with bias + relu, ragged M / N / K; within the
     float64 bar."""
-    assert dense.tile_count("gemm_nt", "bf16x6") == 8
+    assert dense.tile_count("gemm_nt", "bf16x6") == 9
     A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
     At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
     bt = torch.from_numpy(b).to(cuda)
     ref = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6_inloop")
     _check_gemm(ref.cpu().numpy(), A, B, bias=b, relu=True)
-    for tile in range(9):
+    for tile in range(10):
         C = dense.gemm_nt(At, Bt, bias=bt, act="relu", math="bf16x6", tile=tile)
         assert torch.equal(C, ref), tile
 
