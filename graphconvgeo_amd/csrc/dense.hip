@@ -667,6 +667,12 @@ __device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, float* lds_wave
                                            16, voff, 0, 0, 0);
 }
 
+// the same with the non-temporal policy (a stream read once, e.g. the fused layer's A rows)
+__device__ __forceinline__ void blds16_nt(__amdgpu_buffer_rsrc_t r, float* lds_wave_base, int voff) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)(lds_wave_base),
+                                           16, voff, 0, 0, 2);
+}
+
 __device__ __forceinline__ void glds16(const float* src, float* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(reinterpret_cast<glds_src_t>(reinterpret_cast<uintptr_t>(src)),
                                    (glds_dst_t)(lds_wave_base), 16, 0, 0);
@@ -1263,6 +1269,8 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       blds16(rbs, stage + i * 256, voff[u]);
     }
   };
+  // (A keeps the default policy: the N / BN column tiles of a row block re-read its rows from
+  // L2 -- non-temporal A loads measured 3.5-17 % slower, profiles/r05/nontemporal_streams.jsonl)
   auto load_a = [&](int chunk, f4 (&lo)[RT], f4 (&hi)[RT]) {
     const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
 #pragma unroll
@@ -1384,8 +1392,13 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
   if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
+// C is written once and read by the next kernel long after L2 has turned over (840k x 930 =
+// 3.1 GB): non-temporal stores keep the weight planes and the row blocks' A in L2 (K = 300
+// projections +4 %, K = 930 unchanged, profiles/r05/nontemporal_streams.jsonl)
+#define GCG_EPI_NT true
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
+#undef GCG_EPI_NT
 }
 
 // ---------------------------------------------------------------------------------------
@@ -1401,6 +1414,10 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // as 0 (buffer range), A's elements past K are zeroed before the split, W's padding columns
 // are handled by the epilogue's straddle guard. All LDS (ring, row reductions, bias, labels,
 // row weights) is one array: a second __shared__ object makes hipcc drain the DMA queue.
+// Round 5: A (each row read by exactly one workgroup) is DMA'd and the logits gradient stored
+// with the non-temporal policy, so these streams (1 GB in, 3.1 GB out at Twitter-World) stop
+// evicting the weight planes every workgroup re-reads from L2: World 139.4-140.1 -> 147.6-148.6
+// TF (bf16x6), Twitter-US and the f32 forms unchanged (profiles/r05/nontemporal_streams.jsonl).
 // ---------------------------------------------------------------------------------------
 template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0>
 __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused6_kernel(
@@ -1449,7 +1466,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
     float* stage = smem + (chunk & 1) * STAGE;
     const auto ra = brsrc(A + row0 * lda + 32 * chunk, a_bytes - 128 * chunk);
 #pragma unroll
-    for (int u = 0; u < UA; ++u) blds16(ra, stage + (wave + WR * WC * u) * 256, voff[u]);
+    for (int u = 0; u < UA; ++u) blds16_nt(ra, stage + (wave + WR * WC * u) * 256, voff[u]);
   };
   // W: lane offsets (row 4q, column of group g); rows i and 16 + i through the scalar offset
   int bofs[G];
@@ -1659,12 +1676,14 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, B, 1, ldb, colw, j, q);
 #define GCG_EPI_BV_READY
 #define GCG_EPI_LABELS_LDS
+#define GCG_EPI_NT true
   f4 bv[G];
 #pragma unroll
   for (int g = 0; g < G; ++g) bv[g] = *reinterpret_cast<const f4*>(&sbias[colw + 64 * g + 4 * j]);
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
 #undef GCG_EPI_LABELS_LDS
+#undef GCG_EPI_NT
 }
 
 // One wave per row: the row (N <= 256*NV) is read once into registers, then max, sum of
