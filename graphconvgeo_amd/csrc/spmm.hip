@@ -85,10 +85,16 @@ __device__ __forceinline__ Vec<VEC> load_vec_nt(const float* __restrict__ p) {
   return r;
 }
 
+// Round 5: the dwordx4 output rows are stored non-temporal -- Y is written once and read by
+// the next kernel long after L2 has turned over, and the default policy let it evict the gather
+// hint's hot Z rows: World power-law 6.19-6.25 -> 6.15-6.18 ms, uniform 9.20-9.21 -> 9.13-9.16,
+// the Twitter-US step's SpMMs -0.5..-1.3 % (profiles/r05/spmm_nontemporal_y.jsonl). Round 2
+// measured the same change neutral, before the gather hint kept a hot set in L2.
 template <int VEC>
 __device__ __forceinline__ void store_vec(float* __restrict__ p, const Vec<VEC>& v) {
   if constexpr (VEC == 4) {
-    *reinterpret_cast<float4*>(p) = make_float4(v.x[0], v.x[1], v.x[2], v.x[3]);
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    __builtin_nontemporal_store(f4v{v.x[0], v.x[1], v.x[2], v.x[3]}, reinterpret_cast<f4v*>(p));
   } else if constexpr (VEC == 2) {
     *reinterpret_cast<float2*>(p) = make_float2(v.x[0], v.x[1]);
   } else {

@@ -5,7 +5,7 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/r05tab
 mkdir -p $out
-timeout -k 10 600 python -u -m pytest -x -q --tb=short --timeout 300 --timeout-method thread -m gpu tests/test_dense_gpu.py tests/test_mlpconv_gpu.py tests/test_config3_gpu.py tests/test_layers_gpu.py tests/test_bf16x6_numerics.py > $out/tests.log 2>&1 || { grep -E 'Error|assert|FAILED|passed|failed' $out/tests.log | cut -c1-300 | tail -30; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --tb=short --timeout 300 --timeout-method thread -m gpu ${TESTS:-tests/test_dense_gpu.py} tests/test_mlpconv_gpu.py tests/test_config3_gpu.py tests/test_layers_gpu.py tests/test_bf16x6_numerics.py > $out/tests.log 2>&1 || { grep -E 'Error|assert|FAILED|passed|failed' $out/tests.log | cut -c1-300 | tail -30; exit 1; }
 tail -1 $out/tests.log
 for i in 1 2; do
   for order in reference propagate_first; do
