@@ -1419,7 +1419,12 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // evicting the weight planes every workgroup re-reads from L2: World 139.4-140.1 -> 147.6-148.6
 // TF (bf16x6), Twitter-US and the f32 forms unchanged (profiles/r05/nontemporal_streams.jsonl).
 // ---------------------------------------------------------------------------------------
-template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0>
+// CS = 1 (round 5, FX only): the A chunk is split cooperatively -- each of the workgroup's
+// threads splits one 16-B k-quad of one row (BM x 8 quads = the thread count) and writes its
+// three planes to an LDS image ([plane][BM rows][4 slots of 16 B], key nt_key<4>, the NT
+// kernel's conflict-free B image), then every wave reads its RT x 3 plane fragments from it --
+// instead of all WR x WC waves splitting all BM rows in registers; one more barrier per chunk.
+template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0, int CS = 0>
 __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused6_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
@@ -1434,7 +1439,9 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   static_assert(NGA % (WR * WC) == 0, "whole A DMA instructions per wave");
   constexpr int OFF_RED = S * STAGE, OFF_BIAS = OFF_RED + 4 * WC * BM;
   constexpr int OFF_LAB = OFF_BIAS + BN, OFF_RW = OFF_LAB + BM;
-  __shared__ __attribute__((aligned(16))) float smem[OFF_RW + BM];
+  constexpr int OFF_PL = OFF_RW + BM, PL_FLOATS = BM * 16;  // (CS) plane p image at p * PL_FLOATS
+  __shared__ __attribute__((aligned(16))) float smem[OFF_PL + (CS ? 3 * PL_FLOATS : 0)];
+  static_assert(!CS || (FX && BM * 8 == 64 * WR * WC), "CS: one k-quad of one row per thread");
   float (*red)[WC][BM] = reinterpret_cast<float (*)[WC][BM]>(smem + OFF_RED);
   float* sbias = smem + OFF_BIAS;
   int* slab = reinterpret_cast<int*>(smem + OFF_LAB);
@@ -1616,8 +1623,45 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
     const int kc0 = 32 * c;
     const float* stage = smem + (c & 1) * STAGE;
     bf8 ap[RT][3];
+    if constexpr (CS) {
+      // thread (row r = tid / 8, quad kq = tid % 8: k = kc0 + 4 kq .. + 3) splits its 4 floats;
+      // MFMA operand position of k: slot q = kq & 3, half kq >> 2 (low: k = 4q + w, high: 16 +
+      // 4q + w) -- 8 B of the slot per plane
+      const int r = tid >> 3, kq = tid & 7;
+      f4 x = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * (kq ^ (r & 7)));
+      if (kc0 + 32 > K) {
+        const int lim = K - kc0 - 4 * kq;
 #pragma unroll
-    for (int t = 0; t < RT; ++t) {
+        for (int w = 0; w < 4; ++w) x[w] = w < lim ? x[w] : 0.f;
+      }
+      f2 lo2 = {x[0], x[1]}, hi2 = {x[2], x[3]};
+      unsigned pw[3][2];
+      pw[0][0] = split_pair(lo2);
+      pw[0][1] = split_pair(hi2);
+      pw[1][0] = split_pair(lo2);
+      pw[1][1] = split_pair(hi2);
+      pw[2][0] = __builtin_bit_cast(unsigned, __builtin_convertvector(lo2, bf2));
+      pw[2][1] = __builtin_bit_cast(unsigned, __builtin_convertvector(hi2, bf2));
+      const int so = r * 16 + 4 * ((kq & 3) ^ nt_key<4>(r)) + 2 * (kq >> 2);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) {
+        using u2v = __attribute__((ext_vector_type(2))) unsigned;
+        *reinterpret_cast<u2v*>(smem + OFF_PL + p * PL_FLOATS + so) = u2v{pw[p][0], pw[p][1]};
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        const int rr = arow0 + 16 * t;
+        const int ro = rr * 16 + 4 * (q ^ nt_key<4>(rr));
+#pragma unroll
+        for (int p = 0; p < 3; ++p)
+          ap[t][p] = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(smem + OFF_PL + p * PL_FLOATS + ro));
+      }
+    }
+#pragma unroll
+    for (int t = 0; t < (CS ? 0 : RT); ++t) {
       const int r = arow0 + 16 * t;
       const f4 lo = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * (q ^ (r & 7)));
       const f4 hi = *reinterpret_cast<const f4*>(stage + r * 32 + 4 * ((4 + q) ^ (r & 7)));
@@ -2158,16 +2202,21 @@ gcg_status check_opts(const char* fn, int op, int math, int tile) {
 }
 
 // The fused output layer on the bf16 matrix cores (gemm_fused6_kernel). ws != NULL: the weight's
-// planes pre-split into it (FX = 1); tile 0 = 64 rows x 8 waves of 128 columns at N > 768 (the
-// planes read once per 64 rows, half the 32-row form's L2 reads), else 32 rows x 4 waves; tile
-// 1 = the 32-row form at any N (bitwise the in-register split); tile 2 = the 64-row form (N >
-// 768 only). ws == NULL: the weight split in every workgroup's registers, 32 rows x 4 waves.
+// planes pre-split into it (FX = 1); tile 3 = 64 rows x 8 waves of 128 columns at N > 768 (the
+// planes read once per 64 rows, half the 32-row form's L2 reads), else 32 rows x 4 waves, with
+// the A chunk split cooperatively into LDS planes (CS = 1; World 144.5-145.1 -> 152.2-152.8 TF,
+// Twitter-US 117-118 -> 120-122, profiles/r05/fused_cooperative_split.jsonl); tile 0 = tile 3;
+// tile 1 = the 32-row form at any N with every wave splitting A in registers (bitwise the
+// in-register weight split); tile 2 = the 64-row form likewise (N > 768 only). Every CS form is
+// bitwise its CS = 0 form. ws == NULL: the weight split in every workgroup's registers, 32 rows x
+// 4 waves.
 gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, const float* B,
                          int64_t ldb, const float* bias, float* C, int64_t ldc,
                          const int32_t* labels, float scale, const float* scale_dev,
                          float* loss_rows, float* correct_rows, const float* row_w,
                          hipStream_t st, void* ws, int tile) {
   const int g = (N + 255) / 256;
+  if (ws != nullptr && tile == 0) tile = 3;
   if (ws != nullptr) {  // the weight's planes pre-split (FX = 1) for the tile's BN columns
     const int Kc = (K + 31) / 32;
     if (tile == 2 && g != 4)
@@ -2180,10 +2229,21 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
                        bn);
     GCG_HIP_CHECK(hipGetLastError());
     const auto* wsp = static_cast<const unsigned*>(ws);
-    if (wide) {
+    if (wide && tile == 3) {
+      hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 0, 1, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
+                         dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels,
+                         scale, scale_dev, loss_rows, correct_rows, row_w, wsp);
+    } else if (wide) {
       hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 0, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
                          dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels,
                          scale, scale_dev, loss_rows, correct_rows, row_w, wsp);
+    } else if (tile == 3) {  // the 32-row form with the cooperative A split
+      const dim3 grid(static_cast<unsigned>((M + 31) / 32));
+      switch (g) {
+        case 1: hipLaunchKernelGGL((gemm_fused6_kernel<2, 1, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 2: hipLaunchKernelGGL((gemm_fused6_kernel<2, 2, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        default: hipLaunchKernelGGL((gemm_fused6_kernel<2, 3, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+      }
     } else {
       const dim3 grid(static_cast<unsigned>((M + 31) / 32));
       switch (g) {
@@ -2559,7 +2619,7 @@ int32_t gcg_dense_tile_count(int32_t op, int32_t math) {
     case GCG_DENSE_GEMM_NT:
       return math == GCG_MATH_F32 ? kNtTileCount : math == GCG_MATH_BF16X6 ? kNt3TileCount : -1;
     case GCG_DENSE_FUSED:
-      return math == GCG_MATH_F32 ? 5 : math == GCG_MATH_BF16X6 ? 2 : -1;
+      return math == GCG_MATH_F32 ? 5 : math == GCG_MATH_BF16X6 ? 3 : -1;
     case GCG_DENSE_GEMM_TN: return math == GCG_MATH_F32 ? kTnTileCount : -1;
     default: return -1;
   }

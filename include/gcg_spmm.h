@@ -446,9 +446,11 @@ int64_t gcg_gemm_nt_bf16x6_workspace(int64_t N, int64_t K);
  *     into 0 / 2 / 4 / 8 / 16 rotating parts (tile 0: 8 at N > 768, else 4) -- bitwise equal.
  *   GCG_MATH_BF16X6 (gemm_fused6_kernel): ws != NULL (gcg_project_softmax_xent_workspace(N, K,
  *     math) bytes, 16-B aligned): the weight's three bf16 planes split once per call into it;
- *     tile 0 = 64 rows x 8 waves at N > 768 (row sums over 8 column waves), else 32 rows x 4
- *     waves; tile 1 = 32 rows x 4 waves at any N (bitwise the ws == NULL form); tile 2 = the
- *     64-row form (N > 768 only). ws == NULL: the weight split in every workgroup's registers,
+ *     tile 0 = tile 3 = 64 rows x 8 waves at N > 768 (row sums over 8 column waves), else 32
+ *     rows x 4 waves, the A chunk split once per workgroup into LDS planes; tile 1 = 32 rows x 4
+ *     waves at any N (bitwise the ws == NULL form); tile 2 = the 64-row form (N > 768 only);
+ *     tiles 1 / 2 split A in every wave's registers, bitwise equal to tile 3 of their shape.
+ *     ws == NULL: the weight split in every workgroup's registers,
  *     32 rows x 4 waves (tile 0 only). The 64-row form is within f32 rounding of the 32-row one
  *     (another association of the row sums), with the same hits.
  * Legacy entries: gcg_project_softmax_xent_f32 and _weighted_f32 = GCG_MATH_F32, tile 0;

@@ -210,8 +210,9 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     workspace on the 32-row 4-wave tile (tile 1) -- the same products in the same order: bitwise
     equal (gradient, loss, hits, probabilities), rows past M included -- and on the 64-row 8-wave
     tile (tile 2; tile 0 picks it at N > 768), whose row sums run over 8 column waves (another
-    association): within f32 rounding, the same hits."""
-    assert dense.tile_count("fused", "bf16x6") == 2
+    association): within f32 rounding, the same hits. Tile 3 (tile 0's shape with the A chunk
+    split cooperatively into LDS planes) is bitwise the form of that shape."""
+    assert dense.tile_count("fused", "bf16x6") == 3
     P, W, b = _rand((M, K), 51, 0.3), _rand((K, N), 52, 0.3), _rand((N,), 53)
     y = np.random.default_rng(54).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
@@ -238,6 +239,10 @@ def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
         from graphconvgeo_amd._native import NativeError
         with pytest.raises(NativeError):
             run(True, tile=2)  # the 64-row tile needs N > 768
+    # tile 3: tile 0's shape with the cooperative A split -- bitwise the 32-row form at N <= 768,
+    # the 64-row one above
+    for a, r in zip(run(True, tile=3), ref if N <= 768 else wide[1]):
+        assert torch.equal(a, r)
     for G2, l2, h2, p2 in wide:
         assert torch.equal(h2, ref[2])
         assert float((l2 - ref[1]).abs().max()) < 1e-5

@@ -29,7 +29,7 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     logits64 = P[rows].double() @ W.double() + b.double()
     _, l64, h64, G64 = O.softmax_xent_f64(logits64.cpu().numpy(), y[rows].cpu().numpy(), scale=1.0 / T)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    forms = [("bf16x6", t) for t in range(3 if C > 768 else 2)] + [("f32", t) for t in range(6)]
+    forms = [("bf16x6", t) for t in (range(4) if C > 768 else (0, 1, 3))] + [("f32", t) for t in range(6)]
     for math, tile in forms:
       f = lambda: dense._fused(P, Wp, b, y, 1.0 / T, None, G, loss, hits, math=math, tile=tile)  # noqa: E731
       f()
