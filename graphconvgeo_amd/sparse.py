@@ -32,9 +32,18 @@ ACTS = {None: GCG_ACT_NONE, "none": GCG_ACT_NONE, "linear": GCG_ACT_NONE,
 MODES = ("auto", "fast", "ordered", "rowwise")
 
 # 'auto' runs the bitwise 'ordered' plan unless one row is long enough to outlast the
-# whole launch (then rows are split, 'fast'): longest-first scheduling hides a row of up
-# to ~nnz/2048 nonzeros behind the bulk (Twitter-World: 12,189 of 41.4M, measured equal).
-AUTO_SPLIT_RATIO = 2048
+# whole launch (then rows are split, 'fast'). Round 2 set the limit at nnz/2048 (long rows then
+# ran on one wave); since the ordered plan runs long rows on whole workgroups (round 3) and
+# cuts hub rows into column slices (round 5), a row streams at ~19 GB/s per CU against ~6.5
+# TB/s for the launch, i.e. it outlasts the launch only beyond ~nnz/340 (nnz/215 sliced).
+# Round 5: nnz/512. The W1 gradient's tail gather (CSR(X^T) without the dense head, 43.5M
+# nonzeros, longest row 43,164 = nnz/1008) ran 'fast' at 8.28 ms and runs 'ordered' -- bitwise
+# -- at 7.82-7.89 ms (tools/exp_xt_tail.py, profiles/r05/xt_tail_modes.jsonl); Twitter-World
+# H (12,189 of 41.4M) is ordered either way.
+AUTO_SPLIT_RATIO = 512
+# DeviceCSR.tmatmul moves the dense Zipf-head columns to the MFMA GEMM when CSR(X^T)'s longest
+# row exceeds nnz / TMATMUL_SPLIT_RATIO (the round-2 rule, kept for that decision)
+TMATMUL_SPLIT_RATIO = 2048
 # ... and the plan-less 'rowwise' form (also bitwise) when no row is a hub: longest row at most
 # AUTO_ROWWISE_SKEW x the mean, on a graph large enough to fill the chip with one wave per row.
 # Measured on the Twitter-World uniform-degree graph (max 2.2x the mean), K = 300: 9.43 vs
@@ -444,7 +453,7 @@ class DeviceCSR:
         rounding of the gather (a different summation order), not bitwise."""
         T = self.transpose()
         use_split = mode == "fast" or (
-            mode == "auto" and T.max_row_nnz() * AUTO_SPLIT_RATIO > max(T.nnz, 1))
+            mode == "auto" and T.max_row_nnz() * TMATMUL_SPLIT_RATIO > max(T.nnz, 1))
         split = self._dense_column_split() if use_split else None
         if split is None:
             return spmm(T, G, mode=mode, out=out)

@@ -34,3 +34,16 @@ def test_auto_small_graph_keeps_plan():
 def test_auto_one_giant_row_splits():
     indptr = np.concatenate([[0], np.arange(1, 70_001) + 10_000_000])
     assert gs.resolve_auto(_Shape(indptr)) == "fast"
+
+
+def test_auto_long_rows_below_the_launch_stay_ordered():
+    """A longest row of ~nnz/1000 (the W1 gradient's tail gather: 43,164 of 43.5M) runs the
+    bitwise ordered plan (whole-workgroup rows); split only past nnz/AUTO_SPLIT_RATIO."""
+    n = 100_000
+    lens = np.full(n, 400, dtype=np.int64)
+    lens[0] = 40_000  # 40k of ~40M nonzeros
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    assert gs.resolve_auto(_Shape(indptr)) == "ordered"
+    lens[0] = int(indptr[-1]) // gs.AUTO_SPLIT_RATIO + 1000
+    indptr = np.concatenate([[0], np.cumsum(lens)])
+    assert gs.resolve_auto(_Shape(indptr)) == "fast"

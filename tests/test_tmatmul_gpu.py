@@ -102,7 +102,7 @@ def test_tmatmul_auto_keeps_bitwise_when_rows_do_not_split(monkeypatch):
     G = torch.randn(4000, 8, device="cuda")
     T = A.transpose()
     Y = A.tmatmul(G, mode="auto")
-    if T.max_row_nnz() * gs.AUTO_SPLIT_RATIO <= T.nnz:
+    if T.max_row_nnz() * gs.TMATMUL_SPLIT_RATIO <= T.nnz:
         assert "_dense_split" not in A.__dict__
         assert torch.equal(Y, gs.spmm(T, G, mode="ordered"))
     else:
