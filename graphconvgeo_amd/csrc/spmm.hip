@@ -926,15 +926,23 @@ int64_t coop_min_nnz(int64_t task_nnz) { return 8 * task_nnz; }
 // 1.636, P = 8 0.919 / 0.854 / 0.822 / 0.821 (`fast` 7.238 / 1.824 / 0.942 on that box): the
 // rows of 512..4096 nonzeros no longer run on one wave (up to ~0.5 ms each).
 constexpr int64_t kDefaultOrderedTaskNnz = 128;
-int64_t default_task_nnz(int64_t nnz, int ordered) {
-  const int64_t cap = ordered ? kDefaultOrderedTaskNnz : kDefaultTaskNnz;
+// ... and 256 for matrices whose rows average >= 256 nonzeros (the W1 gradient's CSR(X^T) tail:
+// Twitter-US 11.6M nonzeros over 10k rows, ordered 2.21 ms at 128 vs 2.06 at 256 = `fast`;
+// Twitter-World 43.5M over 50k rows 7.86-7.88 either way; profiles/r05/xt_tail_modes.jsonl):
+// with 128, every row from 1,024 nonzeros is a whole-workgroup hand-over row, most of such a
+// matrix.
+constexpr int64_t kLongRowsOrderedTaskNnz = 256;
+int64_t default_task_nnz(int64_t nnz, int ordered, int64_t n_rows) {
+  const bool long_rows = n_rows > 0 && nnz >= 256 * n_rows;
+  const int64_t cap = ordered ? (long_rows ? kLongRowsOrderedTaskNnz : kDefaultOrderedTaskNnz)
+                              : kDefaultTaskNnz;
   int64_t w = nnz / (ordered ? 32768 : 8192);
   return w < 32 ? 32 : (w > cap ? cap : w);
 }
 
 gcg_status build_host_plan(int64_t n_rows, const int32_t* indptr, const int32_t* out_rows,
                            int64_t n_out, int64_t task_nnz, int ordered, HostPlan* hp) {
-  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows], ordered);
+  if (task_nnz <= 0) task_nnz = default_task_nnz(indptr[n_rows], ordered, n_rows);
   if (indptr[0] != 0) return fail(GCG_ERR_BAD_CSR, "indptr[0] = %d != 0", indptr[0]);
   for (int64_t r = 0; r < n_rows; ++r)
     if (indptr[r + 1] < indptr[r]) return fail(GCG_ERR_BAD_CSR, "indptr decreases at row %lld", (long long)r);
@@ -1131,7 +1139,7 @@ gcg_status gcg_spmm_plan_create(gcg_spmm_plan** plan, int64_t n_rows, int64_t n_
   gcg_spmm_plan* p = new (std::nothrow) gcg_spmm_plan();
   if (p == nullptr) return fail(GCG_ERR_ALLOC, "plan allocation failed");
   p->n_rows = n_rows; p->n_cols = n_cols; p->nnz = nnz; p->n_out = n_out;
-  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz, ordered);
+  p->ordered = ordered; p->task_nnz = task_nnz > 0 ? task_nnz : default_task_nnz(nnz, ordered, n_rows);
   p->n_tasks = static_cast<int>(hp.tasks.size() / 4);
   p->n_long = static_cast<int>(hp.longs.size() / 4);
   p->n_coop = static_cast<int>(hp.n_coop);

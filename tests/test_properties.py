@@ -37,8 +37,9 @@ def test_planner_partitions_work_exactly(native_lib, lens, task_nnz, ordered, us
     tasks, longs, nslots = _plan(indptr, task_nnz, int(ordered), rows)
     if task_nnz > 0:
         W = task_nnz
-    elif ordered:  # spmm.hip default_task_nnz: 128 for ordered plans (round 5)
-        W = max(32, min(128, int(indptr[-1]) // 32768))
+    elif ordered:  # spmm.hip default_task_nnz: 128 for ordered plans, 256 at >= 256 per row
+        cap = 256 if n > 0 and int(indptr[-1]) >= 256 * n else 128
+        W = max(32, min(cap, int(indptr[-1]) // 32768))
     else:
         W = max(32, min(512, int(indptr[-1]) // 8192))
     covered = np.zeros(n_out, np.int64)
