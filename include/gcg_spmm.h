@@ -96,7 +96,8 @@ gcg_status gcg_spmm_csr_f32(int64_t n_rows, int64_t n_cols, int64_t nnz,
  * reused for every K. Reads indptr (and out_rows) back to the host once and
  * validates indptr; this call synchronizes `stream` -- it is NOT a hot-path call.
  *   task_nnz  : target nonzeros per wave task (0 = default: clamp(nnz / 8192, 32, 512), ordered
- *               plans clamp(nnz / 32768, 32, 128)).
+ *               plans clamp(nnz / 32768, 32, 128), or up to 256 when rows average >= 256
+ *               nonzeros).
  *   ordered   : 1 = never split a row's sum (bitwise scipy order): rows longer than task_nnz
  *                   are scheduled first, those longer than 8 x task_nnz on a whole workgroup
  *                   each (the storage-order sum handed from wave to wave, still bitwise); one
