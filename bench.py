@@ -230,13 +230,16 @@ def _read_kernel_trace(d: str, kernel: str = PMC_KERNEL):
 
 
 def live_traffic(H, K: int, mode: str, timeout_s: int = 240, keep_dir: str = "",
-                 tag: str = "headline", launches: int = 20) -> dict:
+                 tag: str = "headline", launches: int = 20, warmup: int = 5) -> dict:
     """Measured in this run, before this process touches the GPU, by child processes that replay
     the bench's own SpMM launch (tools/pmc_probe.py: the same graph, empty_dense layout, mode and
     gather hint), each under `timeout -s KILL`:
       1. `rocprofv3 --kernel-trace --stats`: the kernel's average duration on THIS box
-         (`kernel_trace_ms`, over `launches` dispatches after the plan-building one) -- the
-         profile that backs the line's own kernel time (VERDICT r04 item 2);
+         (`kernel_trace_ms`) over the bench's own loop -- `warmup` untimed launches, then
+         `launches` back to back, the dispatches of that timed loop only -- and the probe's wall
+         clock per step over the same loop under the profiler (`traced_ms_per_step`): the
+         profile that backs the line's kernel time, and the profiler's own overhead beside it
+         (VERDICT r05 item 3);
       2. `--pmc FETCH_SIZE`, 3. `--pmc WRITE_SIZE` (separate passes, guide §PMC): HBM-side bytes
          per launch, 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the gfx950 correction of
          MI355X_MICROARCH.md:298), the mean over the launches after the plan-building one.
@@ -258,29 +261,36 @@ def live_traffic(H, K: int, mode: str, timeout_s: int = 240, keep_dir: str = "",
         probe = [sys.executable, os.path.join(ROOT, "tools", "pmc_probe.py"), graph, "--K",
                  str(K), "--mode", mode]
 
-        def run(name, prof_args, n_launch):
+        def run(name, prof_args, n_launch, n_warm=0):
             cmd = (["timeout", "-s", "KILL", str(timeout_s), prof] + prof_args +
                    ["--output-format", "csv", "-d", os.path.join(tmpd, name), "-o", name, "--"] +
-                   probe + ["--launches", str(n_launch)])
+                   probe + ["--launches", str(n_launch), "--warmup", str(n_warm)])
             t1 = time.perf_counter()
             r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout_s + 30)
             print(f"bench: live {name} pass rc={r.returncode} in {time.perf_counter() - t1:.1f} s",
                   file=sys.stderr, flush=True)
             if r.returncode != 0:
                 raise RuntimeError(f"{name} pass rc={r.returncode}: {(r.stderr or r.stdout)[-300:]}")
+            for line in r.stdout.splitlines():
+                if line.startswith("PROBE "):
+                    return json.loads(line[6:])
+            return {}
 
-        # 1. kernel trace: the kernel's own duration on this box
+        # 1. kernel trace: the kernel's own duration on this box, over the bench's loop
         try:
-            run("kt", ["--kernel-trace", "--stats"], launches)
+            n_launch = max(int(launches), 1)
+            probe_rec = run("kt", ["--kernel-trace", "--stats"], n_launch, max(int(warmup), 0))
             ns = _read_kernel_trace(os.path.join(tmpd, "kt"))
-            if len(ns) < 2:
+            if len(ns) < n_launch:
                 raise RuntimeError(f"kernel trace: {len(ns)} {PMC_KERNEL} dispatches")
-            ns = ns[1:]  # drop the plan-building call's launch
+            ns = ns[-n_launch:]  # the timed loop's dispatches (plan + warm-up dropped)
             out["kernel_trace"] = {
                 "avg_ms": round(float(np.mean(ns)) / 1e6, 4),
                 "min_ms": round(min(ns) / 1e6, 4), "max_ms": round(max(ns) / 1e6, 4),
-                "dispatches": len(ns),
-                "source": "rocprofv3 --kernel-trace --stats of tools/pmc_probe.py (this run)"}
+                "dispatches": len(ns), "warmup": max(int(warmup), 0),
+                "traced_ms_per_step": probe_rec.get("ms_per_step"),
+                "source": "rocprofv3 --kernel-trace --stats of tools/pmc_probe.py (this run): "
+                          "the bench's warm-up + timed loop, its timed dispatches"}
             if keep_dir:
                 import glob
                 os.makedirs(keep_dir, exist_ok=True)
@@ -469,8 +479,9 @@ def spmm_mode_variant(A, H, K: int, mode: str, reps: int, dev) -> dict:
 
 
 def spmm_wide_variant(A, N: int, nnz: int, K: int, mode: str, reps: int, dev) -> dict:
-    """the same World SpMM at the wider hidden size K = 1500
-    (tensormain.py:398), on the headline graph already resident in HBM."""
+    """the same World SpMM at a wider hidden size -- K = 500, main_mlpconv's
+    default (tensormain.py:209), or 1500 (tensormain.py:398) -- on the headline graph already
+    resident in HBM."""
     g = torch.Generator(device=dev).manual_seed(SEED + 13)
     Z = gs.empty_dense(N, K, dev).copy_(torch.randn((N, K), generator=g, device=dev))
     Y = gs.empty_dense(N, K, dev)
@@ -513,11 +524,15 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
            "train_rows_distinct": int(np.unique(train).size),
            "data": "synthetic", "data_gen_s": round(t_gen, 1), "steps": steps, "warmup": warmup}
     clf = None
-    for order, graph in (("reference", False), ("propagate_first", False),
-                         ("propagate_first", True)):
-        clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, order=order,
-                      use_graph=graph)
+    # MLPCONV's default order ("auto": propagate-first when C > K) first, under its resolved
+    # name; then the reference's association, and the default captured as a HIP graph
+    for order, graph in ((None, False), ("reference", False), (None, True)):
+        kw = {} if order is None else {"order": order}
+        clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, use_graph=graph, **kw)
         clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H and X
+        if order is None:
+            order = clf.l_out.order
+            out["default_order"] = f"{clf.order} -> {order}"
         y_train = torch.as_tensor(Y[train].astype(np.int32), device=dev)
         clf.n_epochs = 1  # lets _make_train_step capture the epoch when use_graph
         step = clf._make_train_step(LasagneAdam(clf.params), y_train)
@@ -547,6 +562,14 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
     gate = gs.empty_gate(n, K, dev)
     At = A.rows_transpose(rows)
     nnz_t = int(np.diff(H.indptr)[rows.host].sum())
+    # X.W1 and X^T.g gather rows of a small dense operand (W1: F x K = 12 MB at Twitter-US) that
+    # stays in L2 / the Infinity Cache: the edge-centric model counts every gathered row as an HBM
+    # read; SURVEY.md §8d's K2 model counts W1 once -- 4(N+1) + 8 nnz_X + 4FK + 4NK (and, for
+    # X^T.g, G read once and the F x K result written once). What bounds these kernels is neither
+    # HBM figure but the L2 gather rate (16.8-18.8 TB/s)
+    k2 = {"X.W1 (mlpconv.py:71)": 4 * (n + 1) + 8 * X.nnz + 4 * cfg.n_features * K + 4 * n * K,
+          "X^T.g (grad of mlpconv.py:71)": (4 * (cfg.n_features + 1) + 8 * X.nnz + 4 * n * K
+                                            + 4 * cfg.n_features * K)}
     ops = {
         "X.W1 (mlpconv.py:71)": (lambda: gs.spmm(Xd, W1), spmm_bytes(n, X.nnz, K),
                                  "W1 (12 MB) cache-resident"),
@@ -565,6 +588,10 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
         fn()
         k_ms = time_events(fn, max(steps, 5), dev)
         per[name] = {"ms": round(k_ms, 3), "GBps_edge_centric": round(nbytes / (k_ms * 1e-3) / 1e9, 1)}
+        if name in k2:
+            per[name].update(GBps_k2_model=round(k2[name] / (k_ms * 1e-3) / 1e9, 1),
+                             k2_model_bytes=k2[name], bound="L2 gather rate (operand cache-"
+                             "resident; neither byte model is an HBM bound here)")
         if note:
             per[name]["note"] = note
     out["spmm"] = per
@@ -605,6 +632,39 @@ def alternatives(H, rank, world, dev, part, Zl, K, B, eff, gen, timed, reps, arg
             alt[f"exchange_{m}"] = {"error": f"{type(exc).__name__}: {exc}"[:500]}
         torch.cuda.empty_cache()
     return alt
+
+
+def chunks_calibration(part, Zl, Y, K, chunks, ms, eff, timed, reps, args, t_comm, t_sp,
+                       gathered) -> dict:
+    """N > 1, in the headline line: the pipelined step at 1, 2 and 4 column chunks with the
+    headline's own exchange (the same collectives, only narrower), beside what the chunk model
+    predicts for each (distributed.pipeline_time on this run's measured exchange and local SpMM),
+    and the inbound rate per xGMI link the exchange alone achieved -- so one scaling run fixes
+    XGMI_LINK_GBPS and choose_chunks."""
+    from graphconvgeo_amd.distributed import XGMI_LINK_GBPS, pipeline_time
+    world = part.world
+    links = min(world - 1, 7)
+    ab, model = {}, {}
+    for c in (1, 2, 4):
+        model[str(c)] = round(pipeline_time(t_comm, t_sp, c), 4)
+        if c == chunks:
+            ab[str(c)] = round(ms, 4)  # the headline step itself
+            continue
+        if c > 1 and K // c < 16:
+            continue
+        part.chunk_buffers(K, c).fill(Zl)
+
+        def step_c(c=c):
+            part.spmm_pipelined(None, Y, n_chunks=c, mode=eff, task_nnz=args.task_nnz)
+        step_c()
+        ab[str(c)] = round(timed(step_c, reps), 4)
+    best = min(ab, key=lambda k: ab[k])
+    return {"chunks_ab": {"ms_per_step": ab, "model_ms": model, "best": int(best),
+                          "chosen": chunks, "chosen_over_best": round(ab[str(chunks)] / ab[best], 4)
+                          if str(chunks) in ab else None},
+            "xgmi_links": links,
+            "xgmi_link_GBps_fit": round(gathered / (t_comm * 1e-3) / links / 1e9, 2),
+            "xgmi_link_GBps_model": XGMI_LINK_GBPS}
 
 
 def exchange_ab(H, rank, world, dev, part, Zl, K, B, eff, timed, reps, args, m) -> dict:
@@ -673,11 +733,15 @@ def main():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="N > 1 process-group backend (nccl = RCCL over xGMI; gloo only to "
                          "rehearse several ranks on one GPU)")
-    ap.add_argument("--dist-timeout", type=float, default=600.0,
+    ap.add_argument("--dist-timeout", type=float, default=180.0,
                     help="N > 1: seconds a collective may take before the process group "
-                         "aborts and the run exits non-zero (distributed.init_process_group)")
-    ap.add_argument("--no-alternatives", dest="alternatives", action="store_false",
-                    help="N > 1: skip timing the feature-parallel alternative")
+                         "aborts and the run exits non-zero (distributed.init_process_group); "
+                         "well inside the driver's 600 s bench limit")
+    ap.add_argument("--exchange-ab", dest="alternatives", action="store_true",
+                    help="N > 1: after the headline line, time the other exchanges (mesh / "
+                         "halo / all-gather) and the feature-parallel alternative; printed as "
+                         "one 'ALT {...}' line (off by default: the driver's scaling run runs "
+                         "only the headline's own collectives)")
     ap.add_argument("--partitioned", action="store_true",
                     help="use the row-partitioned (all-gather) path even at N = 1")
     args = ap.parse_args()
@@ -705,7 +769,7 @@ def main():
             live = {"error": "skipped: this run is itself under rocprofv3"}
         else:
             live = live_traffic(H, K, host_mode(H, args.mode), keep_dir=args.profile_dir,
-                                tag="headline")
+                                tag="headline", launches=args.steps, warmup=args.warmup)
             if args.variants:
                 H_u = synthetic_graph(cfg.n_nodes, cfg.n_edges, kind="uniform")
                 live_u = live_traffic(H_u, K, host_mode(H_u, args.mode),
@@ -812,12 +876,19 @@ def main():
             kt = live.pop("kernel_trace", None) or {}
             roofline["live_pmc"] = live
             if "avg_ms" in kt:
-                # the same launch under rocprofv3 --kernel-trace, same box, same run: backs the
-                # line's kernel time; a kernel cannot take longer than the step that runs it
+                # the same launch under rocprofv3 --kernel-trace, same box, same run, same loop
+                # (warm-up + timed launches): backs the line's kernel time. A kernel cannot take
+                # longer than the step that runs it -- compared without slack, against this
+                # process's step and against the traced process's own step; their ratio is the
+                # profiler's measured overhead
                 roofline["kernel_trace_ms"] = kt["avg_ms"]
                 roofline["kernel_trace"] = kt
                 roofline["kernel_trace_vs_ms_per_step"] = round(kt["avg_ms"] / ms, 4)
-                roofline["kernel_trace_le_step"] = bool(kt["avg_ms"] <= ms * 1.02)
+                roofline["kernel_trace_le_step"] = bool(kt["avg_ms"] <= ms)
+                tms = kt.get("traced_ms_per_step")
+                if tms:
+                    roofline["kernel_trace_le_traced_step"] = bool(kt["avg_ms"] <= tms)
+                    roofline["profiler_overhead"] = round(tms / ms - 1.0, 4)
             elif kt:
                 roofline["kernel_trace"] = kt
         # compulsory bytes (every array touched once) beside the edge-centric
@@ -867,16 +938,9 @@ def main():
                      "nnz_local": part.nnz_local, "block_rows": part.block_rows,
                      "spmm_only_aggregate_GBps": round(B / (t_sp * 1e-3) / 1e9, 1)}
 
-    # Alternative strategy measured in the same run (N > 1): H replicated, Z split by columns,
-    # no exchange (distributed.FeatureParallelSpMM). Reported beside the row-partitioned value.
-    alt = None
-    if world > 1 and args.alternatives:
-        try:
-            alt = alternatives(H, rank, world, dev, part, Zl, K, B, eff, gen, timed, reps, args)
-        except Exception as exc:  # noqa: BLE001 -- the A/B is an extra: keep the line
-            # (raised on every rank alike -- a bad argument, an unsupported op -- so no rank is
-            # left waiting in a collective)
-            alt = {"error": f"{type(exc).__name__}: {exc}"[:500]}
+        if world > 1:
+            dist_info.update(chunks_calibration(part, Zl, Y, K, chunks, ms, eff, timed, reps,
+                                                args, t_comm, t_sp, gathered))
 
     value = B / (ms * 1e-3) / 1e9
     rec = {
@@ -902,17 +966,19 @@ def main():
         rec["roofline"] = roofline
     if dist_info:
         rec["distributed"] = dist_info
-    if alt:
-        rec["alternatives"] = alt
     if world == 1 and not args.partitioned and args.variants:
         # SURVEY.md §8d second run: uniform degrees (no Infinity-Cache hub reuse)
         del Z, Y
         rec["variants"] = {"uniform": spmm_variant(cfg, "uniform", K, args.mode,
                                                    max(args.steps, 5), dev, H=H_u, live=live_u)}
         H_u = None
-        if args.graph == "powerlaw" and K != 1500:
-            rec["variants"]["k1500"] = spmm_wide_variant(A, N, nnz, 1500, eff,
-                                                         max(args.steps // 4, 3), dev)
+        if args.graph == "powerlaw":
+            # the reference's other hidden sizes on the headline graph: main_mlpconv's default
+            # hidden = 500 (tensormain.py:209) and the tuned 1500 (tensormain.py:398)
+            for kk in (500, 1500):
+                if kk != K:
+                    rec["variants"][f"k{kk}"] = spmm_wide_variant(
+                        A, N, nnz, kk, eff, max(args.steps // (2 if kk < 1000 else 4), 3), dev)
         if eff != "fast":
             # the same SpMM in 'fast' mode (hub rows split, within 1e-5): the N = 1 point of a
             # `--mode fast` scaling series (the default series runs the whole graph's mode,
@@ -931,7 +997,19 @@ def main():
         except Exception as exc:  # informational only
             rec["cpu_multicore"] = {"error": repr(exc)[:200]}
     if rank == 0:
-        print(json.dumps(rec), flush=True)
+        print(json.dumps(rec), flush=True)  # the headline: printed before any extra
+    # Opt-in extras (N > 1, --exchange-ab): the other exchanges (their collectives are not the
+    # headline's) and the feature-parallel alternative, after the line is out: a failure or a
+    # hang there (the process group's --dist-timeout ends it) cannot cost the headline.
+    if world > 1 and args.alternatives:
+        try:
+            alt = alternatives(H, rank, world, dev, part, Zl, K, B, eff, gen, timed, reps, args)
+        except Exception as exc:  # noqa: BLE001 -- the A/B is an extra
+            # (raised on every rank alike -- a bad argument, an unsupported op -- so no rank is
+            # left waiting in a collective)
+            alt = {"error": f"{type(exc).__name__}: {exc}"[:500]}
+        if rank == 0:
+            print("ALT " + json.dumps(alt), flush=True)
     if world > 1:
         import torch.distributed as dist
         dist.destroy_process_group()

@@ -13,9 +13,12 @@ W1, b1, W2, b2 are replicated. Per step:
               logits_p = (H_p . exchange(h_p . W2) + b2)[targets_p]   C wide
               loss_p, hits_p = softmax-CE row kernel
             the mean is over ALL ranks' targets (1/T_total), the penalty is added on rank 0
-  backward  through H's symmetry: the gradient of Y_p = H_p . Z w.r.t. Z, reduced to rank p's
-            rows, is H_p . exchange(g) -- the same exchange and the same local SpMM as the
-            forward (H^T = H, so row block p of H^T is H_p). dW1 = X_p^T . dZ1_p, dW2, db local.
+  backward  the gradient of Y_p = H_p . Z w.r.t. Z, reduced to rank p's rows, is
+            (H^T)_p . exchange(g): for a symmetric H (checked once on the host,
+            distributed.host_is_symmetric) that is H_p -- the same exchange and the same local
+            SpMM as the forward; any other H (the row-normalized D^-1 (A+I) of main.py:451-455)
+            gets a second partition of CSR(H^T) over the same row bounds, Theano's H^T . gz.
+            dW1 = X_p^T . dZ1_p, dW2, db local.
   all-reduce  ONE bucket with every parameter gradient (W1: F x K = 60 MB at Twitter-World,
             W2 1.1 MB, the biases) over RCCL, then the replicated Lasagne-Adam update.
 
@@ -36,7 +39,8 @@ import torch.distributed as dist
 
 from . import dense
 from . import sparse as gs
-from .distributed import RowPartitionedCSR, TargetRows, local_targets  # noqa: F401 (re-export)
+from .distributed import (RowPartitionedCSR, TargetRows, host_is_symmetric,  # noqa: F401
+                          local_targets)
 from .layers import _glorot_uniform, csr_matmul
 from .mlpconv import LasagneAdam
 
@@ -81,13 +85,14 @@ class GPUOps:
 
 class _PartitionedPropagate(torch.autograd.Function):
     """Y_p = act(H_p . exchange(Z_p) + b)[targets_p], the exchange pipelined with the SpMM over
-    column chunks (distributed.pipelined_product). Backward through H's symmetry:
-      no targets: dZ_p = H_p . exchange(g . act')            (same exchange, same SpMM)
-      targets   : dZ_p = H_p[:, D] . exchange(g_D)           (TargetRowsBackward: only the
+    column chunks (distributed.pipelined_product). Backward through part_bwd, the partition of
+    H^T over the same row bounds (part itself when H is symmetric):
+      no targets: dZ_p = (H^T)_p . exchange(g . act')
+      targets   : dZ_p = (H^T)_p[:, D] . exchange(g_D)       (TargetRowsBackward: only the
                   distinct targets' gradient rows travel, only their columns are multiplied)"""
 
     @staticmethod
-    def forward(ctx, Z_p, bias, part: RowPartitionedCSR, act, targets, mode, ops):
+    def forward(ctx, Z_p, bias, part: RowPartitionedCSR, act, targets, mode, ops, part_bwd):
         K = Z_p.shape[1]
         rows = None if targets is None else targets.rows
         n_out = part.n_local if rows is None else rows.n
@@ -102,6 +107,7 @@ class _PartitionedPropagate(torch.autograd.Function):
         part.spmm_pipelined(Z_p.detach(), Y, bias=b, gate=gate, act=act, rows=rows, mode=mode,
                             spmm_into=into)
         ctx.part, ctx.act, ctx.targets, ctx.mode, ctx.ops = part, act, targets, mode, ops
+        ctx.part_bwd = part if part_bwd is None else part_bwd
         ctx.has_bias = bias is not None
         ctx.n_in = Z_p.shape[0]
         ctx.save_for_backward(gate)
@@ -117,7 +123,7 @@ class _PartitionedPropagate(torch.autograd.Function):
             g, g_bias = ctx.ops.relu_backward(gY, gate, bias_grad=want_bias)
         g_Z = None
         if ctx.needs_input_grad[0]:
-            part, ops = ctx.part, ctx.ops
+            part, ops = ctx.part_bwd, ctx.ops
             g = g.contiguous()
             if ctx.targets is not None:
                 g_Z = part.target_backward(ctx.targets).backward(g, ops, mode=ctx.mode)
@@ -131,15 +137,19 @@ class _PartitionedPropagate(torch.autograd.Function):
                 pad = torch.zeros((ctx.n_in, g_Z.shape[1]), dtype=g_Z.dtype, device=g_Z.device)
                 pad[: g_Z.shape[0]] = g_Z
                 g_Z = pad
-        return g_Z, g_bias, None, None, None, None, None
+        return g_Z, g_bias, None, None, None, None, None, None
 
 
-def partitioned_propagate(Z_p, part, bias=None, act=None, targets=None, mode="auto", ops=GPUOps):
+def partitioned_propagate(Z_p, part, bias=None, act=None, targets=None, mode="auto", ops=GPUOps,
+                          part_bwd=None):
     """Differentiable (H . Z + b)[targets] restricted to rank p's rows, Z row-partitioned;
-    targets: None (every local row) or a distributed.TargetRows."""
+    targets: None (every local row) or a distributed.TargetRows. part_bwd: the partition of
+    H^T over part's row bounds for the backward (None: H is symmetric, part serves both)."""
     if targets is not None and not isinstance(targets, TargetRows):
         raise TypeError("targets must be a distributed.TargetRows (every rank's target list)")
-    return _PartitionedPropagate.apply(Z_p, bias, part, act, targets, mode, ops)
+    if part_bwd is not None and not np.array_equal(part_bwd.bounds, part.bounds):
+        raise ValueError("part_bwd must partition H^T over the same row bounds as part")
+    return _PartitionedPropagate.apply(Z_p, bias, part, act, targets, mode, ops, part_bwd)
 
 
 class PartitionTargets(TargetRows):
@@ -184,7 +194,7 @@ class RowPartitionedGCN:
     def __init__(self, H, X, train_indices, y, hidden: int, n_classes: int, rank: int,
                  world: int, device, W1=None, W2=None, order: str = "propagate_first",
                  exchange: str = "auto", mode: str = "auto", regul_coefs=(5e-5, 5e-5),
-                 seed: int = 77, group=None, rng=None):
+                 seed: int = 77, group=None, rng=None, symmetric: Optional[bool] = None):
         if order not in ("reference", "propagate_first"):
             raise ValueError("order must be 'reference' or 'propagate_first'")
         self.rank, self.world, self.group = rank, world, group
@@ -193,6 +203,13 @@ class RowPartitionedGCN:
         self.regul_coefs = tuple(regul_coefs)
         H = sps.csr_matrix(H)
         self.part = RowPartitionedCSR(H, rank, world, self.device, group=group, exchange=exchange)
+        # the backward's operator H^T (Theano's S.dot gradient, mlpconv.py:73,90): H_p itself
+        # for a symmetric H, else a partition of CSR(H^T) over the same row bounds. Every rank
+        # decides from the same host H, so all take the same branch.
+        self.symmetric = host_is_symmetric(H) if symmetric is None else bool(symmetric)
+        self.part_t = None if self.symmetric else RowPartitionedCSR(
+            H.T.tocsr(), rank, world, self.device, group=group, exchange=self.part.exchange,
+            bounds=self.part.bounds)
         self.mode = self.part.resolve_mode(mode)  # one SpMM mode on every rank (the whole graph's)
         start, stop = self.part.start, self.part.stop
         Xc = sps.csr_matrix(X)[start:stop]
@@ -243,7 +260,8 @@ class RowPartitionedGCN:
     # -- forward ------------------------------------------------------------------------
     def _hidden(self):
         Z1 = csr_matmul(self.X_p, self.W1, mode=self.mode)  # S.dot(X_p, W1), mlpconv.py:71
-        return partitioned_propagate(Z1, self.part, self.b1, "relu", None, self.mode)
+        return partitioned_propagate(Z1, self.part, self.b1, "relu", None, self.mode,
+                                     part_bwd=self.part_t)
 
     def local_loss_acc(self, name: str = "train", penalty: bool = True):
         """This rank's share of (mean CE + penalty, accuracy) over all ranks' targets of the
@@ -251,12 +269,13 @@ class RowPartitionedGCN:
         tg = self.targets[name]
         h = self._hidden()
         if self.order == "propagate_first":
-            P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
+            P = partitioned_propagate(h, self.part, None, None, tg, self.mode, part_bwd=self.part_t)
             loss, acc = self.proj.softmax_xent(P, self.W2, self.b2, tg.y, denom=tg.total,
                                                row_weight=tg.weight)
         else:
             Z2 = dense.matmul(h, self.W2)  # T.dot(h, W2), mlpconv.py:88
-            logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode)
+            logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode,
+                                            part_bwd=self.part_t)
             loss, acc = dense.softmax_xent(logits, tg.y, denom=tg.total, row_weight=tg.weight)
         if penalty and self.rank == 0:
             c_out, c_hid = self.regul_coefs  # mlpconv.py:235-243, counted once
@@ -282,15 +301,17 @@ class RowPartitionedGCN:
         tg = self.targets[name]
         h = self._hidden()
         if self.order == "propagate_first" and self.n_classes <= dense.FUSED_MAX_COLS:
-            P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
+            P = partitioned_propagate(h, self.part, None, None, tg, self.mode, part_bwd=self.part_t)
             probs = self.proj.probabilities(P, self.W2, self.b2)
         else:
             if self.order == "propagate_first":
-                P = partitioned_propagate(h, self.part, None, None, tg, self.mode)
+                P = partitioned_propagate(h, self.part, None, None, tg, self.mode,
+                                          part_bwd=self.part_t)
                 logits = dense.matmul(P, self.W2, self.b2)
             else:
                 Z2 = dense.matmul(h, self.W2)
-                logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode)
+                logits = partitioned_propagate(Z2, self.part, self.b2, None, tg, self.mode,
+                                            part_bwd=self.part_t)
             probs = dense.softmax(logits)
         return probs.index_select(0, tg.inverse)
 
@@ -362,7 +383,7 @@ class RowPartitionedMLPCONV:
                  early_stopping_max_down=100000, loss_name="log", nonlinearity="rectify",
                  dtype="float32", device="cuda", seed: Optional[int] = None, mode: str = "auto",
                  model_file: Optional[str] = None, report_k_epoch: int = 10,
-                 order: str = "reference", rank: Optional[int] = None,
+                 order: str = "auto", rank: Optional[int] = None,
                  world: Optional[int] = None, group=None, exchange: str = "auto",
                  network_factory=None):
         if dtype != "float32":

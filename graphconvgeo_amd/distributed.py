@@ -66,6 +66,28 @@ def row_partition(indptr: np.ndarray, parts: int, row_cost: int = 2,
     return np.maximum.accumulate(bounds)
 
 
+def host_is_symmetric(H) -> bool:
+    """H == H^T for a host CSR (every rank holds H: no communication). A canonical symmetric
+    matrix transposes to the same arrays (checked first, linear); otherwise the numeric
+    difference decides (duplicates summed)."""
+    H = sps.csr_matrix(H)
+    if H.shape[0] != H.shape[1]:
+        return False
+    T = H.T.tocsr()
+    if (np.array_equal(H.indptr, T.indptr) and np.array_equal(H.indices, T.indices)
+            and np.array_equal(H.data.view(np.uint8), T.data.view(np.uint8))):
+        return True
+    return (abs(H - T) > 0).nnz == 0
+
+
+def _same_host_csr(a, b) -> bool:
+    a, b = sps.csr_matrix(a), sps.csr_matrix(b)
+    if a.indptr is b.indptr and a.indices is b.indices and a.data is b.data:
+        return a.shape == b.shape
+    return (a.shape == b.shape and a.nnz == b.nnz and np.array_equal(a.indptr, b.indptr)
+            and np.array_equal(a.indices, b.indices) and np.array_equal(a.data, b.data))
+
+
 def remap_columns(cols: np.ndarray, bounds: np.ndarray, block_rows: int) -> np.ndarray:
     """Global column id -> row of the padded all-gathered operand."""
     owner = np.searchsorted(bounds, cols, side="right") - 1
@@ -97,7 +119,7 @@ def _wait(work):
         w.wait()
 
 
-DIST_TIMEOUT_S = 600.0
+DIST_TIMEOUT_S = 180.0  # a collective stuck this long is a hang (well inside a 600 s job limit)
 
 
 def init_process_group(backend: str, device=None, timeout_s: float = DIST_TIMEOUT_S):
@@ -391,6 +413,8 @@ class RowPartitionedCSR:
                  plan: Optional[PartitionPlan] = None):
         if plan is None:
             plan = PartitionPlan(H, world, bounds)
+        elif H is not None and H is not plan.H and not _same_host_csr(H, plan.H):
+            raise ValueError("plan was built for another graph (pass H=None with a plan)")
         elif plan.world != world or (bounds is not None and
                                      not np.array_equal(np.asarray(bounds), plan.bounds)):
             raise ValueError("plan was built for another partition")
@@ -633,7 +657,9 @@ class TargetRowsBackward:
     bytes and the targets' share of the nonzeros."""
 
     def __init__(self, part: RowPartitionedCSR, targets: TargetRows):
-        self.part, self.targets = part, targets
+        # the list itself is not kept: it holds this operator (target_backward's cache), and a
+        # reference back would make a cycle that only the cyclic GC frees (ADVICE r05)
+        self.part = part
         counts = [int(d.size) for d in targets.block_distinct]
         pad = max(max(counts, default=0), 1)
         pos_of = np.full(part.n, -1, dtype=np.int64)
@@ -722,7 +748,7 @@ class FeatureParallelSpMM:
         self.c0, self.c1 = self.bounds[rank]
         if local_spmm is None:
             from .sparse import DeviceCSR, spmm
-            self.A = DeviceCSR.from_scipy(sps.csr_matrix(H), self.device, symmetric=True)
+            self.A = DeviceCSR.from_scipy(sps.csr_matrix(H), self.device)
             self._spmm = spmm
         else:
             self.A = sps.csr_matrix(H)

@@ -15,8 +15,8 @@ Here: torch modules with the same constructor arguments and `get_output_for` /
 epilogue; the dense projection T.dot(h, W) runs on the hand-written f32 MFMA kernels of csrc/dense.hip
 (forward and input gradient on the LDS-DMA NT GEMM, the weight gradient on the split-K
 kernel; the trainer's output layer is one fused MFMA kernel, graphconvgeo_amd.dense). Backward follows Theano's rules: grad of
-S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H for the symmetric H; CSR(X^T) built once on the
-device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
+S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H when H is symmetric -- checked once on the device,
+DeviceCSR.check_symmetric -- else CSR(H^T); CSR(X^T) built once on the device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
 
 `GraphConvLayer` is the name BASELINE.json's north_star uses; it is the generic form.
 Rectify is Theano's 0.5*(x+|x|) in the forward, and its gradient 0.5*g*(1+sgn(x)) in the
@@ -215,9 +215,9 @@ class GraphConvLayer(nn.Module):
         self.device = torch.device(device)
         self.num_inputs = in_features if in_features is not None else _num_inputs(incoming)
         self.num_units = int(num_units)
+        # H^T for the backward: H itself when H is symmetric (declared by its builder, or found
+        # so by DeviceCSR.check_symmetric at the first backward), else the built transpose
         self.H = _as_device_csr(H, self.device)
-        if self.H.symmetric is None:
-            self.H.symmetric = False  # transpose built on demand unless declared symmetric
         w = _glorot_uniform(self.num_inputs, self.num_units, rng) if W is None else W
         self.W = nn.Parameter(_as_tensor(w, (self.num_inputs, self.num_units), self.device))
         if b is None:
@@ -422,9 +422,7 @@ class GCN(nn.Module):
                  device="cuda", W1=None, W2=None, mode: str = "auto", rng=None):
         super().__init__()
         self.device = torch.device(device)
-        Hd = _as_device_csr(H, self.device)
-        if Hd.symmetric is None:
-            Hd.symmetric = True  # D^-1/2 (A+I) D^-1/2 of an undirected graph (tensormain.py:170-180)
+        Hd = _as_device_csr(H, self.device)  # symmetry checked at the first backward
         self.X = _as_device_csr(X, self.device)
         if isinstance(rng, (int, np.integer)):
             # one stream for both layers: W1 then W2 drawn in sequence (an int handed to each

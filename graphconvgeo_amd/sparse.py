@@ -316,9 +316,18 @@ class DeviceCSR:
 
     def transpose(self) -> "DeviceCSR":
         """CSR of A^T built on the device (stable: within a row, entries keep A's order).
-        For a symmetric operator (H, by construction) this is A itself."""
+
+        The gradient of S.dot(A, Z) w.r.t. Z is A^T . gz for ANY A (Theano's Dot grad, the
+        backward of mlpconv.py:73,90). `symmetric` True (declared by a builder that makes A
+        symmetric by construction, graph.build_operator) returns A itself; None (unknown, the
+        default for an uploaded matrix) builds A^T once and checks it against A
+        (check_symmetric): when they hold the same entries, A^T is dropped and A is used -- the
+        D^-1/2 (A+I) D^-1/2 of tensormain.py:170-180 -- otherwise the built transpose serves
+        every backward (the row-normalized D^-1 (A+I) of main.py:451-455)."""
         if self.symmetric:
             return self
+        if self.symmetric is None and self.n_rows == self.n_cols:
+            return self if self.check_symmetric() else self._transpose
         if self._transpose is None:
             out_indptr = torch.empty(self.n_cols + 1, dtype=torch.int32, device=self.device)
             out_indices = torch.empty(self.nnz, dtype=torch.int32, device=self.device)
@@ -337,6 +346,48 @@ class DeviceCSR:
             t._transpose = self
             self._transpose = t
         return self._transpose
+
+    def check_symmetric(self) -> bool:
+        """Is A == A^T? Decided once on the device and stored in `symmetric`: A^T is built
+        (gcg_csr_transpose_f32) and compared with A -- the CSR arrays bit for bit (a canonical,
+        sorted symmetric matrix transposes to the same arrays), else the (row, column, value
+        bits) multisets, so a symmetric matrix in any storage order is recognised. Duplicate
+        entries must match one for one; a matrix symmetric only after summing its duplicates is
+        reported unsymmetric (then its exact transpose is used: still correct). One host sync."""
+        if self.symmetric is not None:
+            return bool(self.symmetric)
+        if self.n_rows != self.n_cols:
+            self.symmetric = False
+            return False
+        self.symmetric = False  # transpose() below builds A^T
+        T = self.transpose()
+        same = (torch.equal(self.indptr, T.indptr) and torch.equal(self.indices, T.indices)
+                and torch.equal(self.data.view(torch.int32), T.data.view(torch.int32))) \
+            or self._same_entries(T)
+        if same:
+            self.symmetric = True
+            T._transpose = None
+            self._transpose = None
+        return same
+
+    def _sorted_entries(self):
+        """(row * n_cols + column, value bits) of every entry, sorted by both."""
+        lens = (self.indptr[1:] - self.indptr[:-1]).to(torch.int64)
+        row = torch.repeat_interleave(torch.arange(self.n_rows, device=self.device), lens,
+                                      output_size=self.nnz)
+        key = row * self.n_cols + self.indices.to(torch.int64)
+        bits = self.data.view(torch.int32)
+        o1 = torch.sort(bits, stable=True).indices
+        o2 = torch.sort(key[o1], stable=True).indices
+        order = o1[o2]
+        return key[order], bits[order]
+
+    def _same_entries(self, other: "DeviceCSR") -> bool:
+        if self.shape != other.shape or self.nnz != other.nnz:
+            return False
+        ka, va = self._sorted_entries()
+        kb, vb = other._sorted_entries()
+        return torch.equal(ka, kb) and torch.equal(va, vb)
 
     def rows_transpose(self, rows: RowSelection) -> "DeviceCSR":
         """CSR of (A[rows])^T, built on the device once per row list and cached: the operator

@@ -83,6 +83,20 @@ def normalize_adjacency(adj, out_dtype=np.float32):
     return H.astype(out_dtype)
 
 
+def row_normalize_l1(adj, out_dtype=np.float32):
+    """The reference's NON-symmetric operator D^-1 (A+I) (main.py:451-456): adjacency with the
+    diagonal set to 1, then sklearn normalize(axis=1, norm='l1') -- every row divided by the
+    sum of its absolute values (in float64), then .astype('float32'). Storage sorted by column."""
+    A = sps.csr_matrix(adj, dtype=np.float64).tolil()
+    A.setdiag(1)
+    A = A.tocsr()
+    A.sort_indices()
+    s = np.add.reduceat(np.abs(A.data), A.indptr[:-1])  # every row holds its diagonal 1
+    rows = np.repeat(np.arange(A.shape[0]), np.diff(A.indptr))
+    H = sps.csr_matrix((A.data / s[rows], A.indices.copy(), A.indptr.copy()), shape=A.shape)
+    return H.astype(out_dtype)
+
+
 # ---------------------------------------------------------------------------------------
 # S.dot(H, Z) -> scipy csr_matvecs (mlpconv.py:71,73,90) + layer epilogue
 # ---------------------------------------------------------------------------------------

@@ -64,10 +64,16 @@ def test_bench_two_ranks_gloo(cuda):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), "bench.py",
            "--gpus", "2", "--config", "twitter-us", "--steps", "3", "--warmup", "1",
-           "--dist-backend", "gloo"]
+           "--dist-backend", "gloo", "--exchange-ab"]
     r = subprocess.run(cmd, cwd=ROOT, capture_output=True, text=True, timeout=500, env=env)
     assert r.returncode == 0, r.stderr[-3000:]
     rec = _json_line(r.stdout)
+    # the headline line is out before any extra: the exchange A/B follows as one 'ALT' line
+    lines = r.stdout.splitlines()
+    head = next(i for i, ln in enumerate(lines) if ln.startswith("{"))
+    alt_at = [i for i, ln in enumerate(lines) if ln.startswith("ALT ")]
+    assert len(alt_at) == 1 and alt_at[0] > head
+    alt = json.loads(lines[alt_at[0]][4:])
     assert rec["n_gpus"] == 2 and rec["config"]["parallelism"] == "row2"
     # one mode for every rank and every N: the whole graph's
     assert rec["config"]["mode_resolution"].startswith("the whole graph")
@@ -77,4 +83,10 @@ def test_bench_two_ranks_gloo(cuda):
     for key in ("exchange", "exchange_ms", "local_spmm_ms", "comm_fraction"):
         assert key in d, key
     assert d["exchange_ms"] > 0 and d["local_spmm_ms"] > 0
-    assert "feature_parallel" in rec["alternatives"]
+    # the chunk-count calibration rides in the headline line (same exchange, 1/2/4 chunks)
+    ab = d["chunks_ab"]
+    assert set(ab["ms_per_step"]) == {"1", "2", "4"} and all(v > 0 for v in ab["ms_per_step"].values())
+    assert set(ab["model_ms"]) == {"1", "2", "4"} and ab["chosen"] == d["chunks"]
+    assert d["xgmi_link_GBps_fit"] > 0 and d["xgmi_links"] == 1
+    assert "alternatives" not in rec
+    assert "feature_parallel" in alt and "exchange_halo" in alt, alt

@@ -190,31 +190,49 @@ class _CPUOps:
         return torch.from_numpy(out)
 
 
-def _prop_worker(rank, world, port, n, e, K, exchange, hi, q):
+def _operator(n, e, nonsym):
+    """The symmetric D^-1/2 (A+I) D^-1/2, or the reference's row-normalized D^-1 (A+I)
+    (main.py:451-456) -- not symmetric."""
+    H = synthetic_graph(n, e)
+    if nonsym:
+        from oracle import gcn_oracle as O
+        A = H.copy()
+        A.data[:] = 1.0
+        H = O.row_normalize_l1(A)
+    return H
+
+
+def _prop_worker(rank, world, port, n, e, K, exchange, hi, nonsym, q):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         from graphconvgeo_amd.dist_train import partitioned_propagate
-        from graphconvgeo_amd.distributed import RowPartitionedCSR, TargetRows
-        H = synthetic_graph(n, e)
+        from graphconvgeo_amd.distributed import RowPartitionedCSR, TargetRows, host_is_symmetric
+        H = _operator(n, e, nonsym)
+        assert host_is_symmetric(H) == (not nonsym)
         rng = np.random.default_rng(11)
         Z = rng.standard_normal((n, K)).astype(np.float32)
         b = rng.standard_normal(K).astype(np.float32)
         targets = rng.integers(0, hi, size=n // 2).astype(np.int32)  # duplicates included
         part = RowPartitionedCSR(H, rank, world, "cpu", local_spmm=_oracle_spmm, exchange=exchange)
         part.chunks_override = 3 if world == 3 else None  # the pipelined form in fwd and bwd
+        part_t = None
+        if nonsym:  # the backward's H^T, partitioned over the same row bounds
+            part_t = RowPartitionedCSR(H.T.tocsr(), rank, world, "cpu", local_spmm=_oracle_spmm,
+                                       exchange=exchange, bounds=part.bounds)
+            part_t.chunks_override = part.chunks_override
         Zp = torch.from_numpy(part.local_rows(Z).copy()).requires_grad_()
         bt = torch.from_numpy(b).requires_grad_()
-        h = partitioned_propagate(Zp, part, bt, "relu", None, ops=_CPUOps)
+        h = partitioned_propagate(Zp, part, bt, "relu", None, ops=_CPUOps, part_bwd=part_t)
         tg = TargetRows(targets, part)  # every kept target, duplicates included
         pos = tg.pos
-        P = partitioned_propagate(h, part, None, None, tg, ops=_CPUOps)
+        P = partitioned_propagate(h, part, None, None, tg, ops=_CPUOps, part_bwd=part_t)
         R = torch.from_numpy(rng.standard_normal((targets.size, K)).astype(np.float32))
         (P * R[torch.from_numpy(pos)]).sum().backward()
-        bwd = part.target_backward(tg)
+        bwd = (part_t or part).target_backward(tg)
         # only the distinct targets' rows travel; the operator keeps only their columns
         assert bwd.layout.counts == [d.size for d in tg.block_distinct]
-        assert bwd.nnz <= part.nnz_local
+        assert bwd.nnz <= (part_t or part).nnz_local
         assert tg._backward_op is bwd  # cached on the list, not on the partition
         out = [None] * world
         dist.all_gather_object(out, (part.start, part.stop, pos, P.detach().numpy(),
@@ -225,22 +243,25 @@ def _prop_worker(rank, world, port, n, e, K, exchange, hi, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("exchange,world", [("allgather", 2), ("halo", 2), ("mesh", 2),
-                                            ("mesh", 3), ("allgather", 3), ("allgather", 4),
-                                            ("halo", 4), ("mesh", 4), ("allgather", 8),
-                                            ("halo", 8), ("mesh", 8)])
-def test_partitioned_propagate_fwd_bwd(exchange, world):
+@pytest.mark.parametrize("exchange,world,nonsym", [
+    ("allgather", 2, False), ("halo", 2, False), ("mesh", 2, False), ("mesh", 3, False),
+    ("allgather", 3, False), ("allgather", 4, False), ("halo", 4, False), ("mesh", 4, False),
+    ("allgather", 8, False), ("halo", 8, False), ("mesh", 8, False),
+    ("allgather", 2, True), ("halo", 3, True), ("mesh", 4, True)])
+def test_partitioned_propagate_fwd_bwd(exchange, world, nonsym):
     """Two stacked partitioned propagates (rectify, then a target-row subset with duplicates)
-    and their backward through H's symmetry: activations and input gradients bitwise equal to
-    the single-process oracle chain; the bias gradient (a cross-rank sum) within fp32. At world
-    4 and 8 the targets lie in the first 40 % of the nodes (the reference's train rows come
-    first): the last ranks hold no target, contribute no rows to the target exchange, and still
-    receive the others'."""
+    and their backward through H^T (H itself for the symmetric operator; a partition of CSR(H^T)
+    over the same bounds for the reference's row-normalized D^-1 (A+I), main.py:451-456):
+    activations and input gradients bitwise equal to the single-process oracle chain; the bias
+    gradient (a cross-rank sum) within fp32. At world 4 and 8 the targets lie in the first 40 %
+    of the nodes (the reference's train rows come first): the last ranks hold no target,
+    contribute no rows to the target exchange, and still receive the others'."""
     from oracle import gcn_oracle as O
     n, e, K = 2500, 16000, 12
     hi = n if world < 4 else int(0.4 * n)
-    (out,) = _run_world(_prop_worker, world, n, e, K, exchange, hi)
-    H = synthetic_graph(n, e)
+    (out,) = _run_world(_prop_worker, world, n, e, K, exchange, hi, nonsym)
+    H = _operator(n, e, nonsym)
+    Ht = H.T.tocsr()  # Theano's S.dot gradient H^T . gz (stable transpose: scipy's order)
     rng = np.random.default_rng(11)
     Z = rng.standard_normal((n, K)).astype(np.float32)
     b = rng.standard_normal(K).astype(np.float32)
@@ -250,9 +271,9 @@ def test_partitioned_propagate_fwd_bwd(exchange, world):
     P = O.spmm_f32(H, h, rows=targets)
     g_h = np.zeros((n, K), np.float32)
     O.scatter_add_f32(g_h, targets, R)
-    g_h = O.spmm_f32(H, g_h)                      # H^T = H
+    g_h = O.spmm_f32(Ht, g_h)
     g_pre = g_h * (h > 0)
-    g_Z = O.spmm_f32(H, g_pre.astype(np.float32))
+    g_Z = O.spmm_f32(Ht, g_pre.astype(np.float32))
     got_P = np.zeros_like(P)
     got_gZ = np.zeros_like(g_Z)
     g_b = np.zeros(K, np.float64)
