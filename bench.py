@@ -524,15 +524,16 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
            "train_rows_distinct": int(np.unique(train).size),
            "data": "synthetic", "data_gen_s": round(t_gen, 1), "steps": steps, "warmup": warmup}
     clf = None
-    # MLPCONV's default order ("auto": propagate-first when C > K) first, under its resolved
-    # name; then the reference's association, and the default captured as a HIP graph
-    for order, graph in ((None, False), ("reference", False), (None, True)):
+    # MLPCONV's default (order "auto": propagate-first when C > K) as "default", then both
+    # layer-2 orders explicitly, then the default captured as a HIP graph
+    for order, graph in ((None, False), ("reference", False), ("propagate_first", False),
+                         (None, True)):
         kw = {} if order is None else {"order": order}
         clf = MLPCONV(n_epochs=0, hidden_layer_size=K, device=dev, seed=1, use_graph=graph, **kw)
         clf.fit(X, train, dev_idx, test_idx, Y, H)  # builds layers, uploads H and X
         if order is None:
-            order = clf.l_out.order
-            out["default_order"] = f"{clf.order} -> {order}"
+            out["default_order"] = f"{clf.order} -> {clf.l_out.order}"
+            order = "default"
         y_train = torch.as_tensor(Y[train].astype(np.int32), device=dev)
         clf.n_epochs = 1  # lets _make_train_step capture the epoch when use_graph
         step = clf._make_train_step(LasagneAdam(clf.params), y_train)

@@ -94,17 +94,24 @@ __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
 // (16-deep steps, step s takes k = k0 + 4q + s, k >= K zeroed): Inf propagates, Inf * 0 and
 // Inf - Inf give NaN, overflow gives Inf -- the f32 MFMA kernel's result for that tile. Finite
 // data of sane range never takes the branch (~1 v_cmp_class per accumulator element).
+// Only the tile's in-range elements count (row < M, column < N): what a kernel
+// computes for its padding rows and columns depends on how it loads padding, and a NaN there
+// must not send every edge tile down the slow f32 path.
 template <int RT, int G>
-__device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4]) {
+__device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4], int64_t M, int N,
+                                               int64_t rowb, int colw, int j, int q) {
   bool bad = false;
 #pragma unroll
   for (int t = 0; t < RT; ++t)
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+    for (int r = 0; r < 4; ++r) {
+      const bool row_in = rowb + 16 * t + 4 * q + r < M;
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) bad |= !__builtin_isfinite(acc[t][g][e][r]);
+        for (int e = 0; e < 4; ++e)
+          bad |= row_in && colw + 64 * g + 4 * j + e < N && !__builtin_isfinite(acc[t][g][e][r]);
+    }
   return __builtin_amdgcn_ballot_w64(bad) != 0;
 }
 // B element (k, column n) at B + n * bn + k * bk (NT: Bt, bn = ldbt, bk = 1; fused: W, bn = 1,
@@ -932,7 +939,7 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     }
   }
   if constexpr (MX != 0) {  // bf16x6: f32 semantics for Inf / huge operands (f32_tile)
-    if (tile_nonfinite<RT, G>(acc))
+    if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))
       f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldb, 1, colw, j, q);
   }
 #define GCG_EPI_BV_READY
@@ -1171,7 +1178,7 @@ gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
         }
       }
   }
-  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
@@ -1389,7 +1396,7 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     step(c, alo, ahi, blo, bhi);
     if (c + 1 < Kc) step(c + 1, blo, bhi, alo, ahi);
   }
-  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 // C is written once and read by the next kernel long after L2 has turned over (840k x 930 =
@@ -1716,7 +1723,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       if (c + 1 < Kc) chunk(c + 1, w1, w0);
     }
   }
-  if (tile_nonfinite<RT, G>(acc))  // f32 semantics for Inf / huge operands (f32_tile)
+  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, B, 1, ldb, colw, j, q);
 #define GCG_EPI_BV_READY
 #define GCG_EPI_LABELS_LDS

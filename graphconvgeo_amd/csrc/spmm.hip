@@ -204,7 +204,7 @@ __device__ __forceinline__ void accumulate_range(int s, int e, const int32_t* __
     Vec<VEC> z[U][NCH];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      if constexpr (HC) {  // experiment: sign bit = cold column -> non-temporal gather
+      if constexpr (HC) {  // gather hint: sign bit = cold column -> non-temporal gather
         const float* zrow = Z + static_cast<int64_t>(c[u] & 0x7fffffff) * ldz;
         if (c[u] < 0) {
 #pragma unroll
@@ -550,16 +550,20 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
   }
   if (blk < n_coop) {  // a whole-workgroup long row or slice of one (uniform across the block)
     __shared__ __attribute__((aligned(16))) float sacc[kWave * VEC * NCH];
+    const int4 t0 = tasks[blk];
     if constexpr (SLC) {
-      const int4 t0 = tasks[blk];
       if (uniform(t0.z) == -4) {  // {position, slice, -4, slices}
         coop_slice<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), uniform(t0.y), uniform(t0.w), indptr,
                                              indices, vals, out_rows, Z, ldz, col, gcol, on, K, Y,
                                              ldy, bias, act, gate, ldgate, sacc);
         return;
       }
+    } else {
+      // a sliced plan launched on a kernel without slices (a narrower K or a dword / dwordx2
+      // gather): slice 0 runs the whole row, the others exit (both used to run it)
+      if (uniform(t0.z) == -4 && uniform(t0.y) != 0) return;
     }
-    coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(tasks[blk].x), indptr, indices, vals, out_rows, Z,
+    coop_row<VEC, NCH, U, WPB, HC, TL>(uniform(t0.x), indptr, indices, vals, out_rows, Z,
                                        ldz, col, gcol, on, K, Y, ldy, bias, act, gate, ldgate,
                                        sacc);
     return;
