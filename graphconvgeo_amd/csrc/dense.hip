@@ -177,32 +177,46 @@ constexpr float kNegInf = -std::numeric_limits<float>::infinity();
 // MFMA layout) with DPP lane swaps -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror,
 // row_mirror -- instead of ds_bpermute shuffles. Every lane of the row ends with the same
 // value (each step combines a and b as op(a, b) in one lane and op(b, a) in its partner).
+// Round 6: each step is ONE DPP-sourced VALU op (v_add_f32_dpp / v_min_i32_dpp / v_max_f32_dpp)
+// instead of a v_mov_b32_dpp and the op -- the row reductions are 64 of the fused epilogue's
+// per-wave steps. update_dpp with bound_ctrl lets the compiler fold the permute into the add /
+// min (every lane of these row-internal permutations is valid, so bound_ctrl never applies).
+// fmaxf keeps canonicalising maxes around a folded permute, so the max is written out: the
+// s_nop 1 covers the VALU-write -> DPP-read hazard the compiler cannot see inside the asm. Same
+// values as the two-instruction forms: a + b == b + a, min / max commute (max over quiet NaNs
+// keeps fmaxf's maxNum: a NaN operand gives the other).
 template <int CTRL>
-__device__ __forceinline__ float dpp_f(float v) {
-  return __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL,
-                                                            0xF, 0xF, false));
+__device__ __forceinline__ float upd_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v),
+                                                               CTRL, 0xF, 0xF, true));
 }
 template <int CTRL>
-__device__ __forceinline__ int dpp_i(int v) {
-  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+__device__ __forceinline__ int upd_i(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xF, 0xF, true);
 }
+#define GCG_MAX_DPP(v, CTRL_ASM)                                                             \
+  asm volatile("s_nop 1\n\tv_max_f32_dpp %0, %1, %1 " CTRL_ASM                              \
+               " row_mask:0xf bank_mask:0xf bound_ctrl:1"                                  \
+               : "=v"(v) : "v"(v))
 __device__ __forceinline__ float row16_max(float v) {
-  v = fmaxf(v, dpp_f<0xB1>(v));
-  v = fmaxf(v, dpp_f<0x4E>(v));
-  v = fmaxf(v, dpp_f<0x141>(v));
-  return fmaxf(v, dpp_f<0x140>(v));
+  GCG_MAX_DPP(v, "quad_perm:[1,0,3,2]");
+  GCG_MAX_DPP(v, "quad_perm:[2,3,0,1]");
+  GCG_MAX_DPP(v, "row_half_mirror");
+  GCG_MAX_DPP(v, "row_mirror");
+  return v;
 }
+#undef GCG_MAX_DPP
 __device__ __forceinline__ float row16_sum(float v) {
-  v = v + dpp_f<0xB1>(v);
-  v = v + dpp_f<0x4E>(v);
-  v = v + dpp_f<0x141>(v);
-  return v + dpp_f<0x140>(v);
+  v = v + upd_f<0xB1>(v);
+  v = v + upd_f<0x4E>(v);
+  v = v + upd_f<0x141>(v);
+  return v + upd_f<0x140>(v);
 }
 __device__ __forceinline__ int row16_min(int v) {
-  v = min(v, dpp_i<0xB1>(v));
-  v = min(v, dpp_i<0x4E>(v));
-  v = min(v, dpp_i<0x141>(v));
-  return min(v, dpp_i<0x140>(v));
+  v = min(v, upd_i<0xB1>(v));
+  v = min(v, upd_i<0x4E>(v));
+  v = min(v, upd_i<0x141>(v));
+  return min(v, upd_i<0x140>(v));
 }
 
 
