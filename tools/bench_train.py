@@ -36,7 +36,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--nnz-per-row", type=int, default=64)
     ap.add_argument("--mode", default="auto")
-    ap.add_argument("--order", default="reference", choices=["reference", "propagate_first", "auto"])
+    ap.add_argument("--order", default="auto", choices=["reference", "propagate_first", "auto"],
+                    help="layer-2 order (default: MLPCONV's own default, auto)")
     ap.add_argument("--graph", action="store_true", help="replay the step as a captured HIP graph")
     ap.add_argument("--nt-math", default=None, choices=["f32", "bf16x6", "bf16x6_inloop"],
                     help="products of the NT GEMMs (dense.NT_MATH)")
@@ -111,7 +112,7 @@ def main():
            "train_rows": len(train), "train_rows_distinct": int(uniq.size),
            "spmm_algorithmic_bytes_per_step": total,
            "spmm_effective_GBps_if_all_time_in_spmm": round(total / (ms * 1e-3) / 1e9, 1),
-           "mode": args.mode, "order": args.order, "hip_graph": args.graph,
+           "mode": args.mode, "order": f"{args.order} -> {clf.l_out.order}", "hip_graph": args.graph,
            "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
            "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
            "theano_backward": args.theano_backward,
