@@ -244,7 +244,7 @@ def live_traffic(H, K: int, mode: str, timeout_s: int = 240, keep_dir: str = "",
          per launch, 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes; the gfx950 correction of
          MI355X_MICROARCH.md:298), the mean over the launches after the plan-building one.
     The bytes are L2->fabric bytes: reads the Infinity Cache serves are counted too (no gfx950
-    TCC counter separates them), so they bound the DRAM bytes from above.
+    TCC counter separates them, profiles/HISTORY.md §3), so they bound the DRAM bytes from above.
     keep_dir: copy the kernel-trace stats CSV there (`<tag>_kernel_stats.csv`)."""
     import shutil
     import subprocess
@@ -567,7 +567,7 @@ def train_step_bench(steps: int, warmup: int, dev, config: str = "twitter-us") -
     # stays in L2 / the Infinity Cache: the edge-centric model counts every gathered row as an HBM
     # read; SURVEY.md §8d's K2 model counts W1 once -- 4(N+1) + 8 nnz_X + 4FK + 4NK (and, for
     # X^T.g, G read once and the F x K result written once). What bounds these kernels is neither
-    # HBM figure but the L2 gather rate (16.8-18.8 TB/s)
+    # HBM figure but the L2 gather rate (16.8-18.8 TB/s, MI355X_MICROARCH.md §Indexed rows)
     k2 = {"X.W1 (mlpconv.py:71)": 4 * (n + 1) + 8 * X.nnz + 4 * cfg.n_features * K + 4 * n * K,
           "X^T.g (grad of mlpconv.py:71)": (4 * (cfg.n_features + 1) + 8 * X.nnz + 4 * n * K
                                             + 4 * cfg.n_features * K)}
@@ -724,7 +724,7 @@ def main():
                     help="N = 1: skip timing the output layer's MFMA kernels")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     # auto chunks: the count minimising a pipeline model of this rank's exchange bytes over
-    # xGMI against its local SpMM, each extra chunk costing the SpMM ~9 %
+    # xGMI against its local SpMM, each extra chunk costing the SpMM ~9 % (profiles/HISTORY.md §4)
     ap.add_argument("--chunks", type=int, default=0,
                     help="N > 1: column chunks of the exchange/SpMM pipeline (1 = no overlap; "
                          "0 = auto, RowPartitionedCSR.choose_chunks)")
@@ -818,7 +818,7 @@ def main():
         Y = gs.empty_dense(part.n_local, K, dev)
         if world > 1:
             # the producer's rows live in the exchange buffers' own slots: the step copies
-            # nothing (DESIGN.md §4), it is the exchange pipelined with the local SpMM
+            # nothing (DESIGN.md §5), it is the exchange pipelined with the local SpMM
             part.chunk_buffers(K, chunks).fill(Zl)
             step_z = None
         else:  # world 1: the local SpMM on Zl itself (no exchange, no copies)

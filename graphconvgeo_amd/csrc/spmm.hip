@@ -478,7 +478,7 @@ __device__ __forceinline__ void coop_row(int p, const int32_t* __restrict__ indp
 // the time. (A chained design -- row chunks on several CUs handing the running sum over
 // through a flag -- was built and measured first: 1.66 ms for the P = 8 block vs 1.04
 // whole-row, its phase that adds stored products being as latency-bound as the gather;
-// DESIGN.md §1.1.) Task {position, slice, -4, slices}. Launches of one chunk (NCH = 1: K <= 256
+// profiles/HISTORY.md §1.1.) Task {position, slice, -4, slices}. Launches of one chunk (NCH = 1: K <= 256
 // at dwordx4) gain nothing from a slice, and the wider-chunk dword / dwordx2 launches (rows
 // whose stride is not a multiple of 4 floats) are not cut: slice 0 runs the whole row, the
 // others exit. Compiled only into the SLC = 1 kernels, which run plans with cut rows: inlined
@@ -535,7 +535,7 @@ __global__ __launch_bounds__(kWave * WPB) void spmm_rows_kernel(
     float* __restrict__ Y, int64_t ldy, const float* __restrict__ bias, int act,
     float* __restrict__ ws, int64_t ldws, uint8_t* __restrict__ gate, int64_t ldgate) {
   // (An XCD-aware block -> task mapping was measured and not kept: a random gather has no
-  // per-XCD locality, and it breaks the longest-first task order)
+  // per-XCD locality, and it breaks the longest-first task order; profiles/HISTORY.md §1.1.)
   const int blk = static_cast<int>(blockIdx.x);
   const int lane = threadIdx.x & (kWave - 1);
   const int panel0 = static_cast<int>(blockIdx.y) * (kWave * VEC * NCH);

@@ -42,7 +42,7 @@ from . import sparse as gs
 from .distributed import (RowPartitionedCSR, TargetRows, host_is_symmetric,  # noqa: F401
                           local_targets)
 from .layers import _glorot_uniform, csr_matmul
-from .mlpconv import LasagneAdam
+from .mlpconv import LasagneAdam, trainer_order
 
 log = logging.getLogger(__name__)
 
@@ -423,9 +423,7 @@ class RowPartitionedMLPCONV:
         if self.hidden_layer_size is None:
             raise ValueError("hidden_layer_size is required")
         out_size = int(np.max(Y)) + 1
-        order = self.order
-        if order == "auto":  # as ConvolutionDenseLayer(order="auto")
-            order = "propagate_first" if out_size > self.hidden_layer_size else "reference"
+        order = trainer_order(self.order, self.hidden_layer_size, out_size)  # as MLPCONV
         W1 = W2 = None
         if self.init_parameters is not None:
             W1, _b1, W2, _b2 = self.init_parameters

@@ -96,7 +96,7 @@ def remap_columns(cols: np.ndarray, bounds: np.ndarray, block_rows: int) -> np.n
 
 # Chunk-count model (round 4, RowPartitionedCSR.choose_chunks). The exchange of column chunk c+1
 # overlaps the local SpMM of chunk c; each extra chunk costs the SpMM ~CHUNK_COST (narrower
-# gathers: 2 chunks x1.06-1.07, 4 chunks x1.26-1.30). Exchange rate: xGMI is a full
+# gathers: 2 chunks x1.06-1.07, 4 chunks x1.26-1.30, profiles/HISTORY.md §4). Exchange rate: xGMI is a full
 # mesh of 7 links per MI355X, ~XGMI_LINK_GBPS each way per link in practice (153.6 GB/s per link
 # both ways together), min(P - 1, 7) of them busy; local SpMM at LOCAL_SPMM_GBPS edge-centric.
 XGMI_LINK_GBPS = 64.0

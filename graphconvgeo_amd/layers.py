@@ -16,7 +16,8 @@ epilogue; the dense projection T.dot(h, W) runs on the hand-written f32 MFMA ker
 (forward and input gradient on the LDS-DMA NT GEMM, the weight gradient on the split-K
 kernel; the trainer's output layer is one fused MFMA kernel, graphconvgeo_amd.dense). Backward follows Theano's rules: grad of
 S.dot(A, Z) w.r.t. Z is A^T . gz (A^T = H when H is symmetric -- checked once on the device,
-DeviceCSR.check_symmetric -- else CSR(H^T); CSR(X^T) built once on the device), grad of Y[idx] is a deterministic scatter-add (duplicates add, tensormain.py:226).
+DeviceCSR.check_symmetric -- else CSR(H^T); CSR(X^T) built once on the device), grad of Y[idx]
+is a deterministic scatter-add (duplicates add, tensormain.py:226).
 
 `GraphConvLayer` is the name BASELINE.json's north_star uses; it is the generic form.
 Rectify is Theano's 0.5*(x+|x|) in the forward, and its gradient 0.5*g*(1+sgn(x)) in the

@@ -95,6 +95,22 @@ class LasagneAdam:
             p.grad = None
 
 
+def trainer_order(order: str, in_size: int, n_classes: int) -> str:
+    """The trainer's layer-2 order for `order="auto"` (the default since round 6): propagate
+    first -- (H . h)[targets] then P . W2 + b2 -- whenever the fused MFMA output layer takes the
+    classes (C <= dense.FUSED_MAX_COLS) or the SpMM is narrower that way (C > K); else the
+    reference association. Propagate-first runs the projection over the distinct targets only
+    (38 % of the nodes at train = 60 % drawn with replacement) where the reference order runs it
+    over every node, so it wins even where its SpMM is wider: measured (bench train_step,
+    tools/bench_train.py; profiles/r06/) Twitter-US (C = 256 < K = 300) 9.43 vs 9.93 ms,
+    Twitter-World (C = 930) 40.2 vs 50.7 ms."""
+    if order != "auto":
+        return order
+    if n_classes <= dense.FUSED_MAX_COLS or n_classes > in_size:
+        return "propagate_first"
+    return "reference"
+
+
 class MLPCONV:
     def __init__(self, n_epochs=10, batch_size=1000, init_parameters=None, complete_prob=False,
                  add_hidden=True, regul_coefs=(5e-5, 5e-5), save_results=False,
@@ -125,10 +141,12 @@ class MLPCONV:
         self.mode = mode
         self.model_file = model_file
         self.report_k_epoch = report_k_epoch
-        # ConvolutionDenseLayer order: reference | propagate_first | auto (default: propagate
-        # first when C > K -- Twitter-World's C = 930 > K = 300: 40.0 vs 50.1 ms per epoch).
-        # Neither order is bitwise to the reference's P (the projection runs on MFMA in its own
-        # k order); both meet the same float64 bars (tests/test_config3_gpu.py).
+        # ConvolutionDenseLayer order: reference | propagate_first | auto (the default,
+        # resolved by trainer_order). Neither order is bitwise to the reference's P (the
+        # projection runs on MFMA in its own k order); both meet the same float64 bars
+        # (tests/test_config3_gpu.py).
+        if order not in ("reference", "propagate_first", "auto"):
+            raise ValueError("order must be 'reference', 'propagate_first' or 'auto'")
         self.order = order
         self.use_graph = use_graph  # replay each epoch's fwd+bwd+adam as one captured HIP graph
         # repeated targets (drawn with replacement) computed once, weighted by multiplicity
@@ -153,7 +171,9 @@ class MLPCONV:
                                                   mode=self.mode, rng=rng)
         self.l_out = ConvolutionDenseLayer(self.l_hid1, H=self.l_hid1.H, num_units=out_size,
                                            W=W2, nonlinearity=None, device=self.device,
-                                           mode=self.mode, rng=rng, order=self.order)
+                                           mode=self.mode, rng=rng,
+                                           order=trainer_order(self.order,
+                                                               self.hidden_layer_size, out_size))
         if self.init_parameters is not None:
             with torch.no_grad():
                 self.l_hid1.b.copy_(torch.as_tensor(self.init_parameters[1]))

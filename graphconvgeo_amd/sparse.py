@@ -69,7 +69,7 @@ def resolve_auto(A) -> str:
 # DeviceCSR.tmatmul: columns at least this dense (fraction of rows) leave the CSR gather for
 # the dense MFMA GEMM -- break-even is ~1.5-2 % (a gathered nonzero ~190 ps, a dense element
 # ~3-9 ps at Twitter-World, round-1 measurements; the head size re-checked in round 2 with
-# tools/exp_hybrid_cols.py); at most HYBRID_MAX_COLS
+# tools/exp_hybrid_cols.py, profiles/HISTORY.md §7); at most HYBRID_MAX_COLS
 # of them (the GEMM's cost grows faster than the gather it saves beyond), and only
 # for matrices of at least HYBRID_MIN_ROWS rows (below that everything is cache-resident).
 HYBRID_MIN_DENSITY = 0.02
@@ -319,7 +319,7 @@ class DeviceCSR:
 
         The gradient of S.dot(A, Z) w.r.t. Z is A^T . gz for ANY A (Theano's Dot grad, the
         backward of mlpconv.py:73,90). `symmetric` True (declared by a builder that makes A
-        symmetric by construction, graph.build_operator) returns A itself; None (unknown, the
+        symmetric by construction, graph.normalize_edges_device) returns A itself; None (unknown, the
         default for an uploaded matrix) builds A^T once and checks it against A
         (check_symmetric): when they hold the same entries, A^T is dropped and A is used -- the
         D^-1/2 (A+I) D^-1/2 of tensormain.py:170-180 -- otherwise the built transpose serves

@@ -1,5 +1,5 @@
 """Host-side layout rule of the dense operands (sparse.row_stride / empty_dense's row stride):
-16-B aligned rows whose gathered K floats span the fewest 128-B lines (DESIGN.md §2)."""
+16-B aligned rows whose gathered K floats span the fewest 128-B lines (DESIGN.md §3)."""
 import math
 
 import pytest
