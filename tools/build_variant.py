@@ -22,6 +22,7 @@ def main():
     ap.add_argument("out")
     ap.add_argument("-D", action="append", default=[])
     ap.add_argument("--patch", default=None)
+    ap.add_argument("--flag", action="append", default=[], help="extra hipcc flag (every TU)")
     a = ap.parse_args()
     with tempfile.TemporaryDirectory(prefix="gcg_var_") as tmpd:
         csrc = os.path.join(tmpd, "pkg", "csrc")  # common.h includes ../../include/gcg_spmm.h
@@ -36,7 +37,7 @@ def main():
                     raise SystemExit(f"patch text not found in {fn}: {old[:80]!r}")
                 open(p, "w").write(s.replace(old, new))
         objs = []
-        flags = [*_build.HIPCC_FLAGS, f'-DGCG_SOURCE_HASH="variant"', *[f"-D{d}" for d in a.D]]
+        flags = [*_build.HIPCC_FLAGS, f'-DGCG_SOURCE_HASH="variant"', *[f"-D{d}" for d in a.D], *a.flag]
         procs = []
         for src in _build.SOURCES:
             name = os.path.basename(src)
