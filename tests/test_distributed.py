@@ -565,3 +565,55 @@ def test_target_rows_backward_operator_structure():
         assert op.nnz < part.nnz_local
     # bunched targets: the exact-count mesh is chosen over the padded all-gather
     assert op.layout.method == "mesh"
+
+
+def test_host_symmetry_check():
+    """distributed.host_is_symmetric: the symmetric D^-1/2 (A+I) D^-1/2 (canonical, and with
+    every row's storage order shuffled) is symmetric; the reference's row-normalized
+    D^-1 (A+I) (main.py:451-456) is not; a rectangular matrix never is."""
+    import scipy.sparse as sps
+    from graphconvgeo_amd.distributed import host_is_symmetric
+    H = synthetic_graph(2000, 12000)
+    assert host_is_symmetric(H)
+    Hs = H.copy()
+    rng = np.random.default_rng(0)
+    for i in range(Hs.shape[0]):
+        a, b = Hs.indptr[i], Hs.indptr[i + 1]
+        p = rng.permutation(b - a) + a
+        Hs.indices[a:b], Hs.data[a:b] = Hs.indices[p].copy(), Hs.data[p].copy()
+    assert host_is_symmetric(Hs)
+    assert not host_is_symmetric(_operator(2000, 12000, True))
+    assert not host_is_symmetric(sps.random(20, 30, 0.2, format="csr", dtype=np.float32))
+
+
+def test_plan_of_another_graph_is_refused():
+    """RowPartitionedCSR(H, plan=...) used plan.H silently; a plan built from
+    another graph is now an error (the same graph, as another object, is accepted)."""
+    from graphconvgeo_amd.distributed import PartitionPlan, RowPartitionedCSR
+    H1, H2 = synthetic_graph(1500, 8000), synthetic_graph(1500, 8000, seed=5)
+    plan = PartitionPlan(H1, 2)
+    with pytest.raises(ValueError):
+        RowPartitionedCSR(H2, 0, 2, "cpu", local_spmm=_oracle_spmm, plan=plan)
+    part = RowPartitionedCSR(H1.copy(), 0, 2, "cpu", local_spmm=_oracle_spmm, plan=plan)
+    assert part.plan is plan
+    assert RowPartitionedCSR(None, 1, 2, "cpu", local_spmm=_oracle_spmm, plan=plan).start == plan.bounds[1]
+
+
+def test_target_backward_operator_freed_with_its_list():
+    """the backward operator is cached on the target list and holds no reference
+    back to it, so dropping the list frees both by reference counting (no cycle for the GC)."""
+    import gc
+    import weakref
+    from graphconvgeo_amd.distributed import RowPartitionedCSR, TargetRows
+    H = synthetic_graph(1500, 8000)
+    part = RowPartitionedCSR(H, 0, 2, "cpu", local_spmm=_oracle_spmm, exchange="allgather")
+    tg = TargetRows(np.arange(0, 600, 3, dtype=np.int32), part)
+    op = part.target_backward(tg)
+    assert tg._backward_op is op and not hasattr(op, "targets")
+    ref_op, ref_tg = weakref.ref(op), weakref.ref(tg)
+    gc.disable()
+    try:
+        del op, tg
+        assert ref_tg() is None and ref_op() is None
+    finally:
+        gc.enable()
