@@ -24,6 +24,12 @@ ARCH = os.environ.get("GCG_OFFLOAD_ARCH", "gfx950")
 # -ffp-contract=off: every product and sum is rounded separately, as scipy's csr_matvecs does.
 HIPCC_FLAGS = ["-O3", "-std=c++17", "-ffp-contract=off", "-fPIC", f"--offload-arch={ARCH}",
                "-Wall", "-Wno-unused-command-line-argument"]
+# Per-file extra flags. dense.hip: no SLP vectorizer (round 6) -- it packed the NT GEMM's
+# epilogue (bias add, rectify) and fallback arithmetic into v_pk_add_f32 / v_pk_mul_f32, and a
+# packed f32 op beside another workgroup's MFMAs on the same SIMD costs far more than its issue
+# slot (MI355X_MICROARCH.md, "price of one filler beside MFMAs"): the bf16x6 projection 167 ->
+# 183-185 TF, dP 167 -> 175 on one box, bitwise the same results (profiles/r06/dense_ab.jsonl).
+FILE_FLAGS = {"dense.hip": ["-fno-slp-vectorize"]}
 
 
 def _hipcc() -> str:
@@ -44,6 +50,8 @@ def source_hash() -> str:
         with open(p, "rb") as f:
             h.update(os.path.basename(p).encode() + b"\0" + f.read() + b"\0")
     h.update(" ".join(HIPCC_FLAGS).encode())
+    for name in sorted(FILE_FLAGS):
+        h.update((name + ":" + " ".join(FILE_FLAGS[name])).encode())
     return h.hexdigest()[:16]
 
 
@@ -74,7 +82,8 @@ def build_native(force: bool = False, verbose: bool = False) -> str:
 
         def compile_one(src_obj):
             src, obj = src_obj
-            cmd = [hipcc, *HIPCC_FLAGS, f'-DGCG_SOURCE_HASH="{digest}"', "-c", "-o", obj, src]
+            cmd = [hipcc, *HIPCC_FLAGS, *FILE_FLAGS.get(os.path.basename(src), []),
+                   f'-DGCG_SOURCE_HASH="{digest}"', "-c", "-o", obj, src]
             if src.endswith(".cpp"):
                 cmd = [hipcc, "-x", "hip", *cmd[1:]]
             if verbose:

@@ -42,7 +42,8 @@ def main():
         for src in _build.SOURCES:
             name = os.path.basename(src)
             obj = os.path.join(tmpd, name + ".o")
-            cmd = [_build._hipcc(), *flags, "-c", "-o", obj, os.path.join(csrc, name)]
+            cmd = [_build._hipcc(), *flags, *_build.FILE_FLAGS.get(name, []), "-c", "-o", obj,
+                   os.path.join(csrc, name)]
             if name.endswith(".cpp"):
                 cmd = [cmd[0], "-x", "hip", *cmd[1:]]
             procs.append(subprocess.Popen(cmd))
