@@ -50,14 +50,22 @@ def test_opcheck_dense(cuda):
                           (P, W, b, y, 257, None, True), test_utils=OPCHECK)
 
 
+@pytest.mark.parametrize("operator", ["symmetric", "rownorm"])
 @pytest.mark.parametrize("order", ["reference", "propagate_first"])
-def test_compiled_gcn_forward_backward_bitwise_eager(cuda, order):
+def test_compiled_gcn_forward_backward_bitwise_eager(cuda, order, operator):
     """Reference order with C > K (here 40 > 32): eager runs layers._TransformPropagate (the
     re-associated backward) and the compiled graph its registered twin gcg::transform_propagate,
-    built from the same kernels -- bitwise equal, forward and every gradient."""
+    built from the same kernels -- bitwise equal, forward and every gradient. Also on the
+    reference's non-symmetric row-normalized operator (main.py:451-456), whose backward runs
+    through CSR(H^T) in both forms."""
     import torch._dynamo as dynamo
 
     H, X, idx, W1, W2 = _problem()
+    if operator == "rownorm":
+        from oracle import gcn_oracle as O
+        A = H.copy()
+        A.data[:] = 1.0
+        H = O.row_normalize_l1(A)
     model = GCN(H, X, 200, 32, 40, device=cuda, W1=W1, W2=W2, mode="ordered")
     model.l_out.order = order
     rows = gs.RowSelection(idx, cuda)
@@ -77,4 +85,5 @@ def test_compiled_gcn_forward_backward_bitwise_eager(cuda, order):
     for p, ge in zip(model.parameters(), g_eager):
         assert torch.equal(p.grad, ge)
     assert sum(counters["graph_break"].values()) == 0
+    assert model.l_hid1.H.symmetric is (operator == "symmetric")
     dynamo.reset()
