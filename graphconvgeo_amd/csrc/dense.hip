@@ -94,23 +94,25 @@ __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
 // (16-deep steps, step s takes k = k0 + 4q + s, k >= K zeroed): Inf propagates, Inf * 0 and
 // Inf - Inf give NaN, overflow gives Inf -- the f32 MFMA kernel's result for that tile. Finite
 // data of sane range never takes the branch (~1 v_cmp_class per accumulator element).
-// Only the tile's in-range elements count (row < M, column < N): what a kernel
-// computes for its padding rows and columns depends on how it loads padding, and a NaN there
-// must not send every edge tile down the slow f32 path.
-template <int RT, int G>
-__device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4], int64_t M, int N,
-                                               int64_t rowb, int colw, int j, int q) {
+// Padding rows never count: every kernel clamps the rows it loads past M (and NT kernels the
+// weight rows past N) to the last valid one, so a padding row is non-finite only when a valid
+// row is. MASKCOL: only columns < N count -- for the fused layer's in-register weight split
+// (FX = 0), whose last vector reads the weight's padding columns [N, round4(N)), which may hold
+// anything (a NaN there must not send the tile down the slow f32 path); every other
+// kernel reads zeros or clamped columns past N and keeps the one-compare-per-element check (the
+// masked form costs the fused layer ~2 % at the end of its K loop, PMC r06).
+template <int RT, int G, bool MASKCOL = false>
+__device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4], int N, int colw, int j) {
   bool bad = false;
 #pragma unroll
-  for (int t = 0; t < RT; ++t)
+  for (int g = 0; g < G; ++g)
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const bool row_in = rowb + 16 * t + 4 * q + r < M;
+    for (int e = 0; e < 4; ++e) {
+      const bool col_in = !MASKCOL || colw + 64 * g + 4 * j + e < N;
 #pragma unroll
-      for (int g = 0; g < G; ++g)
+      for (int t = 0; t < RT; ++t)
 #pragma unroll
-        for (int e = 0; e < 4; ++e)
-          bad |= row_in && colw + 64 * g + 4 * j + e < N && !__builtin_isfinite(acc[t][g][e][r]);
+        for (int r = 0; r < 4; ++r) bad |= col_in && !__builtin_isfinite(acc[t][g][e][r]);
     }
   return __builtin_amdgcn_ballot_w64(bad) != 0;
 }
@@ -953,7 +955,7 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     }
   }
   if constexpr (MX != 0) {  // bf16x6: f32 semantics for Inf / huge operands (f32_tile)
-    if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))
+    if (tile_nonfinite<RT, G>(acc, N, colw, j))
       f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldb, 1, colw, j, q);
   }
 #define GCG_EPI_BV_READY
@@ -1192,7 +1194,7 @@ gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
         }
       }
   }
-  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
+  if (tile_nonfinite<RT, G>(acc, N, colw, j))  // f32 semantics for Inf / huge operands
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 #include "gemm_epilogue.inc"
@@ -1410,7 +1412,7 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
     step(c, alo, ahi, blo, bhi);
     if (c + 1 < Kc) step(c + 1, blo, bhi, alo, ahi);
   }
-  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
+  if (tile_nonfinite<RT, G>(acc, N, colw, j))  // f32 semantics for Inf / huge operands
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
 // C is written once and read by the next kernel long after L2 has turned over (840k x 930 =
@@ -1737,7 +1739,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       if (c + 1 < Kc) chunk(c + 1, w1, w0);
     }
   }
-  if (tile_nonfinite<RT, G>(acc, M, N, row0 + wr * 16 * RT, colw, j, q))  // f32 semantics
+  if (tile_nonfinite<RT, G, FX == 0>(acc, N, colw, j))  // f32 semantics (see tile_nonfinite)
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, B, 1, ldb, colw, j, q);
 #define GCG_EPI_BV_READY
 #define GCG_EPI_LABELS_LDS

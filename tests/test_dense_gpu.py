@@ -153,11 +153,15 @@ def test_fused_labels_outside_classes(cuda, N, math, monkeypatch):
 
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (20, 3, 61), (9, 4, 522),
                                    (40, 50, 300), (70, 300, 600)])
-@pytest.mark.parametrize("math", ["bf16x6", "f32"])
-def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N, math, monkeypatch):
+@pytest.mark.parametrize("math,presplit", [("bf16x6", True), ("bf16x6", False), ("f32", True)])
+def test_fused_nan_weight_padding_never_leaks(cuda, M, K, N, math, presplit, monkeypatch):
     """W's padding columns [N, ldw) may hold anything (gcg_spmm.h): NaN there must not reach
-    the softmax sum, the loss or the gradient -- bitwise the zero-padded result."""
+    the softmax sum, the loss or the gradient -- bitwise the zero-padded result. presplit False:
+    the bf16x6 form that splits W in registers and so reads its padding columns; its non-finite
+    check looks at columns < N only, so the NaN does not send the tile down the f32 path
+     -- which would change its bits."""
     monkeypatch.setattr(dense, "FUSED_MATH", math)
+    monkeypatch.setattr(dense, "FUSED_PRESPLIT", presplit)
     P, W, b = _rand((M, K), 31, 0.3), _rand((K, N), 32, 0.3), _rand((N,), 33)
     y = np.random.default_rng(34).integers(0, N, M).astype(np.int32)
     Pt, Wt, bt = (torch.from_numpy(v).to(cuda) for v in (P, W, b))
