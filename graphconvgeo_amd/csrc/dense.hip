@@ -103,6 +103,23 @@ __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
 // masked form costs the fused layer ~2 % at the end of its K loop, PMC r06).
 template <int RT, int G, bool MASKCOL = false>
 __device__ __forceinline__ bool tile_nonfinite(const f4 (&acc)[RT][G][4], int N, int colw, int j) {
+  if constexpr (!MASKCOL) {
+    // x * 0 is 0 for finite x and NaN for Inf / NaN: one packed FMA per two accumulators
+    // (round 6: the fused layer +2 % against a v_cmp_class per accumulator and the SGPR ors;
+    // profiles/r06/dense_ab.jsonl)
+    f2 s = {0.f, 0.f};
+    const f2 z = {0.f, 0.f};
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          s = __builtin_elementwise_fma(f2{acc[t][g][e][0], acc[t][g][e][1]}, z, s);
+          s = __builtin_elementwise_fma(f2{acc[t][g][e][2], acc[t][g][e][3]}, z, s);
+        }
+    return __builtin_amdgcn_ballot_w64(s[0] != s[0] || s[1] != s[1]) != 0;
+  }
   bool bad = false;
 #pragma unroll
   for (int g = 0; g < G; ++g)
@@ -1534,6 +1551,20 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
     slab[r] = y;
     srw[r] = (row_w != nullptr && row < M) ? row_w[row] : 1.f;
   }
+  __syncthreads();
+  // the bias is the accumulators' starting value (b + sum of products), so the epilogue adds
+  // nothing per element; columns past N start at 0 and become -inf in the epilogue (round 6:
+  // +3 %, every wave of the CU's one workgroup runs the epilogue with the matrix pipe idle)
+#pragma unroll
+  for (int g = 0; g < G; ++g) {
+    const f4 bb = *reinterpret_cast<const f4*>(&sbias[colw + 64 * g + 4 * j]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float b0 = colw + 64 * g + 4 * j + e < N ? bb[e] : 0.f;
+#pragma unroll
+      for (int t = 0; t < RT; ++t) acc[t][g][e] = f4{b0, b0, b0, b0};
+    }
+  }
 
   const int ngv = min(G, max(0, (N - colw + 63) / 64));  // groups with a column < N
   const int arow0 = wr * 16 * RT + j;
@@ -1739,10 +1770,23 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       if (c + 1 < Kc) chunk(c + 1, w1, w0);
     }
   }
-  if (tile_nonfinite<RT, G, FX == 0>(acc, N, colw, j))  // f32 semantics (see tile_nonfinite)
+  if (tile_nonfinite<RT, G, FX == 0>(acc, N, colw, j)) {  // f32 semantics (see tile_nonfinite)
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, B, 1, ldb, colw, j, q);
+#pragma unroll
+    for (int g = 0; g < G; ++g)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = colw + 64 * g + 4 * j + e;
+        const float b0 = c < N ? sbias[c] : 0.f;
+#pragma unroll
+        for (int t = 0; t < RT; ++t)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) acc[t][g][e][r] += b0;
+      }
+  }
 #define GCG_EPI_BV_READY
 #define GCG_EPI_LABELS_LDS
+#define GCG_EPI_BIAS_IN_ACC
 #define GCG_EPI_NT true
   f4 bv[G];
 #pragma unroll
@@ -1750,6 +1794,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
 #include "gemm_epilogue.inc"
 #undef GCG_EPI_BV_READY
 #undef GCG_EPI_LABELS_LDS
+#undef GCG_EPI_BIAS_IN_ACC
 #undef GCG_EPI_NT
 }
 
