@@ -352,7 +352,8 @@ def roofline_record(kbytes: int, k_ms: float, traffic, traffic_src: str, kernel:
 
 
 def time_events(fn, reps: int, dev) -> float:
-    """Mean per-call ms of fn() with HIP events on the current stream (fn launches there)."""
+    """Per-call ms of fn() with HIP events on the current stream (fn launches there): the median
+    of the calls, so one host-side hiccup between an event and its launch does not move it."""
     stream = torch.cuda.current_stream(dev)
     evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(reps)]
@@ -361,7 +362,7 @@ def time_events(fn, reps: int, dev) -> float:
         fn()
         b.record(stream)
     torch.cuda.synchronize(dev)
-    return float(np.mean([a.elapsed_time(b) for a, b in evs]))
+    return float(np.median([a.elapsed_time(b) for a, b in evs]))
 
 
 def host_mode(H, mode: str) -> str:
@@ -409,7 +410,7 @@ def spmm_variant(cfg, kind: str, K: int, mode: str, reps: int, dev, H=None, live
 def dense_kernels_bench(reps: int, dev) -> dict:
     """The output layer's MFMA kernels (T.dot(h, W2) + b2, softmax-CE and their gradients,
     mlpconv.py:88-95) at Twitter-World's shapes -- 840k target rows x K=300 x C=930 -- each
-    timed alone with HIP events (mean of `reps` launches after one warm-up), TFLOP/s against
+    timed alone with HIP events (median of `reps` launches after one warm-up), TFLOP/s against
     the dense f32 MFMA peak (steady state: 5 untimed launches first). Random data; parity is
     in tests/test_dense_gpu.py."""
     import math
@@ -838,9 +839,15 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    # HIP events on the SpMM's stream bracket the timed launches themselves: at N = 1 their
+    # span / steps is the line's kernel time (the same launches the wall clock times)
+    stream = torch.cuda.current_stream(dev)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
+    ev0.record(stream)
     for _ in range(args.steps):
         step()
+    ev1.record(stream)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -855,7 +862,8 @@ def main():
     roofline = None
     if args.steps > 0:
         if world == 1 and not args.partitioned:
-            kstep, kbytes = step, B
+            kstep, kbytes = None, B
+            k_ms = ev0.elapsed_time(ev1) / args.steps
         else:
             full_k = part.all_gather(Zl)
             kbytes = spmm_bytes(part.n_local, part.nnz_local, K)
@@ -863,7 +871,7 @@ def main():
             def kstep():
                 gs.spmm(part.A, full_k, out=Y, mode=eff, task_nnz=args.task_nnz)
             kstep()
-        k_ms = time_events(kstep, args.steps, dev)
+            k_ms = time_events(kstep, args.steps, dev)
         traffic = traffic_src = None
         if kbytes == B:
             if live and "traffic" in live:
@@ -890,6 +898,10 @@ def main():
                 if tms:
                     roofline["kernel_trace_le_traced_step"] = bool(kt["avg_ms"] <= tms)
                     roofline["profiler_overhead"] = round(tms / ms - 1.0, 4)
+                    roofline["kernel_trace_note"] = (
+                        "two processes, one box: the trace is bounded by the traced process's "
+                        "own step (kernel_trace_le_traced_step); profiler_overhead = that step / "
+                        "this step - 1 is the measured gap between the processes")
             elif kt:
                 roofline["kernel_trace"] = kt
         # compulsory bytes (every array touched once) beside the edge-centric
