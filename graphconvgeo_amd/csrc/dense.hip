@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstring>
 #include <limits>
+#include <type_traits>
 
 #include "common.h"
 
@@ -83,6 +84,45 @@ __device__ __forceinline__ void split3(const f8 x, bf8& h0, bf8& h1, bf8& h2) {
 }
 __device__ __forceinline__ f4 mfma_bf(bf8 a, bf8 b, f4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// The six plane products of one A fragment (planes a[0] a[1] a[2]) and one B fragment (b0 b1
+// b2) into c, smallest planes first. A lane's 32-deep fragment holds k = kc0 + 4q + i (low
+// half, elements 0-3) and kc0 + 16 + 4q + i (high half). TP = the packed K tail (round 6): a
+// chunk with r = K - kc0 <= 16 live k has both fragments' high halves zero, so every MFMA
+// carries two plane products instead -- the high half holding another plane of the low half's
+// k: a2b0 + a1b1, a0b2 + a1b0, a0b1 + a0b0, 3 MFMAs instead of 6. K = 300 ends in such a chunk
+// (12 live k): the projection and the fused layer issue 57 MFMAs per output tile, not 60.
+// The A side is packed once per chunk in place (pack_tail_a: the same three registers per
+// fragment), the B side per slot. Every bf16x6 kernel packs the same way (bitwise equal).
+// Kernels take the packed tail as a template flag the host sets from K, and peel the last
+// chunk out of the K loop: a runtime branch between the two MFMA paths inside one kernel
+// doubled the register pressure (100s of VGPRs spilled). Measured (one box, three rounds,
+// profiles/r06/tail_packed_fence_ab.jsonl): NT projection 191.4 -> 199.0 TF, dP 179.7 ->
+// 183.5 TF, fused layer unchanged (its last chunk waits on the weight-plane loads).
+__device__ __forceinline__ bf8 lohi(bf8 lo, bf8 hi) {
+  return __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 8, 9, 10, 11);
+}
+__device__ __forceinline__ void pack_tail_a(bf8 (&a)[3]) {
+  const bf8 a0 = a[0], a1 = a[1], a2 = a[2];
+  a[0] = lohi(a2, a1);
+  a[1] = lohi(a0, a1);
+  a[2] = lohi(a0, a0);
+}
+template <bool TP>
+__device__ __forceinline__ f4 mfma6(const bf8 (&a)[3], bf8 b0, bf8 b1, bf8 b2, f4 c) {
+  if constexpr (TP) {  // a packed by pack_tail_a
+    c = mfma_bf(a[0], lohi(b0, b1), c);
+    c = mfma_bf(a[1], lohi(b2, b0), c);
+    return mfma_bf(a[2], lohi(b1, b0), c);
+  } else {
+    c = mfma_bf(a[2], b0, c);
+    c = mfma_bf(a[1], b1, c);
+    c = mfma_bf(a[0], b2, c);
+    c = mfma_bf(a[1], b0, c);
+    c = mfma_bf(a[0], b1, c);
+    return mfma_bf(a[0], b0, c);
+  }
 }
 
 // f32 semantics for the bf16x6 kernels (round 5). Three bf16 planes cannot carry an infinite
@@ -754,6 +794,7 @@ __global__ __launch_bounds__(64 * WR * WC, (NtCfg<RT, G, WR, WC, S, KC>::OCC)) v
 gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                const float* __restrict__ Bt, int64_t ldb, const float* __restrict__ bias, int act,
                float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
+  constexpr bool TP = (MX & 2) != 0;  // the packed K tail (mfma6; MX & 1: bf16x6)
   using Cfg = NtCfg<RT, G, WR, WC, S, KC>;
   constexpr int EPI = 0;  // plain epilogue only (gemm_epilogue.inc names the EPI = 1 operands)
   const int32_t* labels = nullptr;
@@ -891,7 +932,9 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 #pragma unroll
   for (int c = 0; c < S - 1; ++c)
     if (c < n_chunks) issue(c);
-  for (int c = 0; c < n_chunks; ++c) {
+  // one chunk; tp: the packed K tail (mfma6), only the peeled last chunk of a TP kernel (MX & 2,
+  // chosen by the host when that chunk holds <= 16 live k)
+  auto chunk_body = [&](int c, auto tp) {
     // retire this chunk's DMA (leave the later stages in flight), then one barrier
     if constexpr (S == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -913,7 +956,7 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       read_step(stage, 0, af, bf);
       if (kc0 + 16 > K) mask_step(af, bf, kc0);
       mfma_step(af, bf);
-    } else if constexpr (MX == 1) {
+    } else if constexpr ((MX & 1) != 0) {
       // bf16x6: the chunk's two 16-deep fragment sets are one 32-deep bf16 MFMA operand (lane
       // (j, q) holds k = kc0 + 4q + {0..3} and kc0 + 16 + 4q + {0..3}, the same for A and B)
       f4 af0[RT], bf0[G][4], af1[RT], bf1[G][4];
@@ -928,25 +971,26 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                       af1[t][0], af1[t][1], af1[t][2], af1[t][3]};
         split3(x, ap[t][0], ap[t][1], ap[t][2]);
       }
+      auto mm = [&](auto tp) {  // tp: the packed K tail (mfma6)
+        constexpr bool TPC = decltype(tp)::value;
 #pragma unroll
-      for (int g = 0; g < G; ++g)
+        for (int g = 0; g < G; ++g)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const f8 y = {bf0[g][e][0], bf0[g][e][1], bf0[g][e][2], bf0[g][e][3],
-                        bf1[g][e][0], bf1[g][e][1], bf1[g][e][2], bf1[g][e][3]};
-          bf8 b0, b1, b2;
-          split3(y, b0, b1, b2);
+          for (int e = 0; e < 4; ++e) {
+            const f8 y = {bf0[g][e][0], bf0[g][e][1], bf0[g][e][2], bf0[g][e][3],
+                          bf1[g][e][0], bf1[g][e][1], bf1[g][e][2], bf1[g][e][3]};
+            bf8 b0, b1, b2;
+            split3(y, b0, b1, b2);
 #pragma unroll
-          for (int t = 0; t < RT; ++t) {  // smallest planes first
-            f4 c = acc[t][g][e];
-            c = mfma_bf(ap[t][2], b0, c);
-            c = mfma_bf(ap[t][1], b1, c);
-            c = mfma_bf(ap[t][0], b2, c);
-            c = mfma_bf(ap[t][1], b0, c);
-            c = mfma_bf(ap[t][0], b1, c);
-            acc[t][g][e] = mfma_bf(ap[t][0], b0, c);
+            for (int t = 0; t < RT; ++t)
+              acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
           }
-        }
+      };
+      if constexpr (decltype(tp)::value) {
+#pragma unroll
+        for (int t = 0; t < RT; ++t) pack_tail_a(ap[t]);
+      }
+      mm(tp);
     } else if constexpr (PF) {
       // both 16-deep steps' fragments first: the second step's LDS reads are in flight
       // during the first step's MFMAs (counted lgkmcnt waits)
@@ -970,7 +1014,10 @@ gemm_nt_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
         mfma_step(af, bf);
       }
     }
-  }
+  };
+  const int n_full = TP ? n_chunks - 1 : n_chunks;
+  for (int c = 0; c < n_full; ++c) chunk_body(c, std::false_type{});
+  if constexpr (TP) chunk_body(n_full, std::true_type{});
   if constexpr (MX != 0) {  // bf16x6: f32 semantics for Inf / huge operands (f32_tile)
     if (tile_nonfinite<RT, G>(acc, N, colw, j))
       f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldb, 1, colw, j, q);
@@ -1050,7 +1097,7 @@ struct Nt3Cfg {
   static_assert(S >= 2 && S <= 4, "2..4 stages");
 };
 
-template <int RT, int G, int WR, int WC, int S>
+template <int RT, int G, int WR, int WC, int S, bool TP = false>  // TP: the packed K tail
 __global__ __launch_bounds__(64 * WR * WC, (Nt3Cfg<RT, G, WR, WC, S>::OCC)) void
 gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                 const unsigned* __restrict__ Bs, const float* __restrict__ Bt, int64_t ldbt, const float* __restrict__ bias, int act,
@@ -1157,7 +1204,8 @@ gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
   const int brow0 = wc * G * 64 + j;
   for (int c = 0; c < S - 1; ++c)
     if (c < Kc) issue(c);
-  for (int c = 0; c < Kc; ++c) {
+  // one chunk; tp: the packed K tail (mfma6), only the peeled last chunk of a TP kernel
+  auto chunk_body = [&](int c, auto tp) {
     if constexpr (S == 2) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
@@ -1190,27 +1238,31 @@ gemm_nt3_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       split3(x, ap[t][0], ap[t][1], ap[t][2]);
     }
     const float* bsec = stage + Cfg::A_FLOATS;
+    auto mm = [&](auto tp) {  // tp: the packed K tail (mfma6)
+      constexpr bool TPC = decltype(tp)::value;
 #pragma unroll
-    for (int g = 0; g < G; ++g)
+      for (int g = 0; g < G; ++g)
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int rb = brow0 + 64 * g + 16 * e;
-        const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
-        const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
-        const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
-        const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
+        for (int e = 0; e < 4; ++e) {
+          const int rb = brow0 + 64 * g + 16 * e;
+          const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
+          const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
+          const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
+          const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {  // smallest planes first
-          f4 cc = acc[t][g][e];
-          cc = mfma_bf(ap[t][2], b0, cc);
-          cc = mfma_bf(ap[t][1], b1, cc);
-          cc = mfma_bf(ap[t][0], b2, cc);
-          cc = mfma_bf(ap[t][1], b0, cc);
-          cc = mfma_bf(ap[t][0], b1, cc);
-          acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
+          for (int t = 0; t < RT; ++t)
+            acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
         }
-      }
-  }
+    };
+    if constexpr (decltype(tp)::value) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) pack_tail_a(ap[t]);
+    }
+    mm(tp);
+  };
+  const int n_full = TP ? Kc - 1 : Kc;
+  for (int c = 0; c < n_full; ++c) chunk_body(c, std::false_type{});
+  if constexpr (TP) chunk_body(n_full, std::true_type{});
   if (tile_nonfinite<RT, G>(acc, N, colw, j))  // f32 semantics for Inf / huge operands
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
 #define GCG_EPI_BV_READY
@@ -1247,6 +1299,7 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
                  float* __restrict__ Cout, int64_t ldc, int n_col_tiles) {
   using Cfg = Nt3rCfg<RT, G, WR, WC>;
   constexpr bool PL = (V & 1) != 0;
+  constexpr bool TP = (V & 2) != 0;
   constexpr int EPI = 0;
   const int32_t* labels = nullptr;
   float scale = 0.f;
@@ -1345,7 +1398,9 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
   }
 
   const int brow0 = wc * G * 64 + j;
-  auto step = [&](int c, f4 (&lo)[RT], f4 (&hi)[RT], f4 (&nlo)[RT], f4 (&nhi)[RT]) {
+  // tp: the packed K tail (mfma6) -- only the peeled last chunk of a TP kernel
+  auto step = [&](int c, f4 (&lo)[RT], f4 (&hi)[RT], f4 (&nlo)[RT], f4 (&nhi)[RT], auto tp) {
+    constexpr bool TPC = decltype(tp)::value;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // chunk c: its A registers and B planes
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
@@ -1381,53 +1436,61 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
       }
       split3(x, ap[t][0], ap[t][1], ap[t][2]);
     }
-    if constexpr (PL) {
+    auto mm = [&](auto tp) {  // tp: the packed K tail (mfma6)
+      constexpr bool TPC = decltype(tp)::value;
+      if constexpr (PL) {
 #pragma unroll
-      for (int ge = 0; ge < 4 * G; ++ge) {
-        if (ge + 1 < 4 * G) rd_planes(ge + 1, bq[(ge + 1) & 1]);
-        __builtin_amdgcn_sched_barrier(0);
-        const int g = ge >> 2, e = ge & 3;
-        const bf8 (&bb)[3] = bq[ge & 1];
+        for (int ge = 0; ge < 4 * G; ++ge) {
+          if (ge + 1 < 4 * G) rd_planes(ge + 1, bq[(ge + 1) & 1]);
+          __builtin_amdgcn_sched_barrier(0);
+          const int g = ge >> 2, e = ge & 3;
+          const bf8 (&bb)[3] = bq[ge & 1];
 #pragma unroll
-        for (int t = 0; t < RT; ++t) {  // smallest planes first
-          f4 cc = acc[t][g][e];
-          cc = mfma_bf(ap[t][2], bb[0], cc);
-          cc = mfma_bf(ap[t][1], bb[1], cc);
-          cc = mfma_bf(ap[t][0], bb[2], cc);
-          cc = mfma_bf(ap[t][1], bb[0], cc);
-          cc = mfma_bf(ap[t][0], bb[1], cc);
-          acc[t][g][e] = mfma_bf(ap[t][0], bb[0], cc);
+          for (int t = 0; t < RT; ++t)
+            acc[t][g][e] = mfma6<TPC>(ap[t], bb[0], bb[1], bb[2], acc[t][g][e]);
         }
+        return;
       }
-      return;
+#pragma unroll
+      for (int g = 0; g < G; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rb = brow0 + 64 * g + 16 * e;
+          const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
+          const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
+          const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
+          const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
+#pragma unroll
+          for (int t = 0; t < RT; ++t)
+            acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
+        }
+    };
+    if constexpr (TPC) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) pack_tail_a(ap[t]);
     }
-#pragma unroll
-    for (int g = 0; g < G; ++g)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int rb = brow0 + 64 * g + 16 * e;
-        const int so = rb * 16 + 4 * (q ^ nt_key<4>(rb));
-        const bf8 b0 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + so));
-        const bf8 b1 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + Cfg::P_FLOATS + so));
-        const bf8 b2 = __builtin_bit_cast(bf8, *reinterpret_cast<const f4*>(bsec + 2 * Cfg::P_FLOATS + so));
-#pragma unroll
-        for (int t = 0; t < RT; ++t) {
-          f4 cc = acc[t][g][e];
-          cc = mfma_bf(ap[t][2], b0, cc);
-          cc = mfma_bf(ap[t][1], b1, cc);
-          cc = mfma_bf(ap[t][0], b2, cc);
-          cc = mfma_bf(ap[t][1], b0, cc);
-          cc = mfma_bf(ap[t][0], b1, cc);
-          acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
-        }
-      }
+    mm(tp);
   };
   f4 alo[RT], ahi[RT], blo[RT], bhi[RT];
   issue_b(0);
   load_a(0, alo, ahi);
-  for (int c = 0; c < Kc; c += 2) {
-    step(c, alo, ahi, blo, bhi);
-    if (c + 1 < Kc) step(c + 1, blo, bhi, alo, ahi);
+  // TP (V & 2, chosen by the host when the last chunk holds <= 16 live k): the loop runs the
+  // full chunks and the last one is peeled, packed (no branch between two MFMA paths in one
+  // kernel: that doubled the register pressure and spilled)
+  const int Kf = TP ? Kc - 1 : Kc;
+  for (int c = 0; c < Kf; c += 2) {
+    step(c, alo, ahi, blo, bhi, std::false_type{});
+    if (c + 1 < Kf) step(c + 1, blo, bhi, alo, ahi, std::false_type{});
+  }
+  if constexpr (TP) {
+    if (Kf & 1) {  // the tail's A arrived in the second set
+#pragma unroll
+      for (int t = 0; t < RT; ++t) {
+        alo[t] = blo[t];
+        ahi[t] = bhi[t];
+      }
+    }
+    step(Kf, alo, ahi, blo, bhi, std::true_type{});
   }
   if (tile_nonfinite<RT, G>(acc, N, colw, j))  // f32 semantics for Inf / huge operands
     f32_tile<RT, G>(acc, M, N, K, A, lda, row0 + wr * 16 * RT, Bt, ldbt, 1, colw, j, q);
@@ -1464,7 +1527,8 @@ gemm_nt3r_kernel(int M, int N, int K, const float* __restrict__ A, int64_t lda,
 // three planes to an LDS image ([plane][BM rows][4 slots of 16 B], key nt_key<4>, the NT
 // kernel's conflict-free B image), then every wave reads its RT x 3 plane fragments from it --
 // instead of all WR x WC waves splitting all BM rows in registers; one more barrier per chunk.
-template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0, int CS = 0>
+// TP: the packed K tail (mfma6): the last chunk peeled, packed (host: when it holds <= 16 k).
+template <int RT, int G, int WR = 1, int WC = 4, int SB = 0, int FX = 0, int CS = 0, bool TP = false>
 __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused6_kernel(
     int M, int N, int K, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
     int64_t ldb, const float* __restrict__ bias, float* __restrict__ Cout, int64_t ldc,
@@ -1573,7 +1637,9 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   if constexpr (!FX) {
     if (ngv > 0) load_w(0, 0, w0);
   }
-  auto group = [&](int c, int g, const bf8 (&ap)[RT][3], const f4 (&w)[8], f4 (&wn)[8]) {
+  // (tp in the group forms below: the packed K tail, mfma6)
+  auto group = [&](int c, int g, const bf8 (&ap)[RT][3], const f4 (&w)[8], f4 (&wn)[8], auto tp) {
+    constexpr bool TPC = decltype(tp)::value;
     // prefetch the next group (or the next chunk's first) into the other set
     if (g + 1 < ngv) load_w(c, g + 1, wn);
     else if (c + 1 < Kc && ngv > 0) load_w(c + 1, 0, wn);
@@ -1583,21 +1649,15 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       bf8 b0, b1, b2;
       split3(y, b0, b1, b2);
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        f4 cc = acc[t][g][e];
-        cc = mfma_bf(ap[t][2], b0, cc);
-        cc = mfma_bf(ap[t][1], b1, cc);
-        cc = mfma_bf(ap[t][0], b2, cc);
-        cc = mfma_bf(ap[t][1], b0, cc);
-        cc = mfma_bf(ap[t][0], b1, cc);
-        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
-      }
+      for (int t = 0; t < RT; ++t)
+        acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
     }
   };
   // SB = 1 (one W register set, for tiles whose accumulators leave no room for two): the next
   // group's loads go into the set as soon as its last column slot is split, so they fly during
   // that slot's MFMAs and the other waves' work
-  auto group_sb = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&w)[8]) {
+  auto group_sb = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&w)[8], auto tp) {
+    constexpr bool TPC = decltype(tp)::value;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const f8 y = {w[0][e], w[1][e], w[2][e], w[3][e], w[4][e], w[5][e], w[6][e], w[7][e]};
@@ -1608,15 +1668,8 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
         else if (c + 1 < Kc && ngv > 0) load_w(c + 1, 0, w);
       }
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        f4 cc = acc[t][g][e];
-        cc = mfma_bf(ap[t][2], b0, cc);
-        cc = mfma_bf(ap[t][1], b1, cc);
-        cc = mfma_bf(ap[t][0], b2, cc);
-        cc = mfma_bf(ap[t][1], b0, cc);
-        cc = mfma_bf(ap[t][0], b1, cc);
-        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
-      }
+      for (int t = 0; t < RT; ++t)
+        acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
     }
   };
   // FX = 1: W's bf16 planes pre-split into a workspace [BN][Kc][3][32] (split3_rows_kernel, zero
@@ -1642,22 +1695,16 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   // one register set, refilled slot by slot: once slot e's MFMAs are issued its registers take
   // the next group's (or the next chunk's first group's) slot e, so each load has three slots
   // of MFMAs (and the other waves' work) to land in
-  auto group_fx = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&wp)[12]) {
+  auto group_fx = [&](int c, int g, const bf8 (&ap)[RT][3], f4 (&wp)[12], auto tp) {
+    constexpr bool TPC = decltype(tp)::value;
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       const bf8 b0 = __builtin_bit_cast(bf8, wp[3 * e]);
       const bf8 b1 = __builtin_bit_cast(bf8, wp[3 * e + 1]);
       const bf8 b2 = __builtin_bit_cast(bf8, wp[3 * e + 2]);
 #pragma unroll
-      for (int t = 0; t < RT; ++t) {
-        f4 cc = acc[t][g][e];
-        cc = mfma_bf(ap[t][2], b0, cc);
-        cc = mfma_bf(ap[t][1], b1, cc);
-        cc = mfma_bf(ap[t][0], b2, cc);
-        cc = mfma_bf(ap[t][1], b0, cc);
-        cc = mfma_bf(ap[t][0], b1, cc);
-        acc[t][g][e] = mfma_bf(ap[t][0], b0, cc);
-      }
+      for (int t = 0; t < RT; ++t)
+        acc[t][g][e] = mfma6<TPC>(ap[t], b0, b1, b2, acc[t][g][e]);
       if (g + 1 < ngv) load_slot(c, g + 1, e, wp);
       else if (c + 1 < Kc && ngv > 0) load_slot(c + 1, 0, e, wp);
     }
@@ -1666,7 +1713,7 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   // one chunk; wa holds its first group's W on entry. G even: the next chunk's first group
   // ends in wa again, G odd (G = 1, 3): in wb, so the loop alternates the sets (a wave whose
   // live-group count has the other parity -- it straddles N -- moves it)
-  auto chunk = [&](int c, f4 (&wa)[8], f4 (&wb)[8]) {
+  auto chunk = [&](int c, f4 (&wa)[8], f4 (&wb)[8], auto tp) {
     // A(c) landed. FX with live groups: the last 12 loads issued (this chunk's first group of
     // planes, prefetched by the previous chunk's last group or the prologue) may still fly
     if (FX && ngv > 0) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
@@ -1730,19 +1777,26 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
       }
       split3(x, ap[t][0], ap[t][1], ap[t][2]);
     }
+    auto groups = [&](auto tp) {
 #pragma unroll
-    for (int g = 0; g < G; ++g) {
-      if (g >= ngv) break;  // wave-uniform: groups wholly past N
-      if constexpr (FX) {
-        group_fx(c, g, ap, wpl);
-      } else if constexpr (SB) {
-        group_sb(c, g, ap, wa);
-      } else if (g % 2 == 0) {
-        group(c, g, ap, wa, wb);
-      } else {
-        group(c, g, ap, wb, wa);
+      for (int g = 0; g < G; ++g) {
+        if (g >= ngv) break;  // wave-uniform: groups wholly past N
+        if constexpr (FX) {
+          group_fx(c, g, ap, wpl, tp);
+        } else if constexpr (SB) {
+          group_sb(c, g, ap, wa, tp);
+        } else if (g % 2 == 0) {
+          group(c, g, ap, wa, wb, tp);
+        } else {
+          group(c, g, ap, wb, wa, tp);
+        }
       }
+    };
+    if constexpr (decltype(tp)::value) {
+#pragma unroll
+      for (int t = 0; t < RT; ++t) pack_tail_a(ap[t]);
     }
+    groups(tp);
     // the last live group (ngv - 1) prefetched the next chunk's first into wb when ngv is odd
     if (!SB && !FX && ngv > 0 && c + 1 < Kc) {
       const bool in_b = (ngv & 1) != 0;
@@ -1762,12 +1816,21 @@ __global__ __launch_bounds__(64 * WR * WC, WR * WC == 4 ? 2 : 1) void gemm_fused
   if constexpr (FX) {
     if (ngv > 0) load_p(0, 0, wpl);
   }
+  const int Kf = TP ? Kc - 1 : Kc;  // full chunks; TP: the last one peeled, packed
   if constexpr (G % 2 == 0 || SB || FX) {
-    for (int c = 0; c < Kc; ++c) chunk(c, w0, w1);
+    for (int c = 0; c < Kf; ++c) chunk(c, w0, w1, std::false_type{});
+    if constexpr (TP) chunk(Kf, w0, w1, std::true_type{});
   } else {
-    for (int c = 0; c < Kc; c += 2) {
-      chunk(c, w0, w1);
-      if (c + 1 < Kc) chunk(c + 1, w1, w0);
+    for (int c = 0; c < Kf; c += 2) {
+      chunk(c, w0, w1, std::false_type{});
+      if (c + 1 < Kf) chunk(c + 1, w1, w0, std::false_type{});
+    }
+    if constexpr (TP) {
+      if (Kf & 1) {  // the tail's first group arrived in the second set
+#pragma unroll
+        for (int i = 0; i < 8; ++i) w0[i] = w1[i];
+      }
+      chunk(Kf, w0, w1, std::true_type{});
     }
   }
   if (tile_nonfinite<RT, G, FX == 0>(acc, N, colw, j)) {  // f32 semantics (see tile_nonfinite)
@@ -2278,6 +2341,16 @@ gcg_status check_opts(const char* fn, int op, int math, int tile) {
 // in-register weight split); tile 2 = the 64-row form likewise (N > 768 only). Every CS form is
 // bitwise its CS = 0 form. ws == NULL: the weight split in every workgroup's registers, 32 rows x
 // 4 waves.
+// a gemm_fused6_kernel launch with the packed K tail when the last chunk holds <= 16 k (needs
+// K in scope); TARGS is the parenthesised template argument list
+#define GCG_FUSED6_UNPAREN(...) __VA_ARGS__
+#define GCG_FUSED6_LAUNCH(TARGS, ...)                                                           \
+  do {                                                                                        \
+    if (K - 32 * ((K - 1) / 32) <= 16)                                                       \
+      hipLaunchKernelGGL((gemm_fused6_kernel<GCG_FUSED6_UNPAREN TARGS, true>), __VA_ARGS__);  \
+    else                                                                                      \
+      hipLaunchKernelGGL((gemm_fused6_kernel<GCG_FUSED6_UNPAREN TARGS>), __VA_ARGS__);        \
+  } while (0)
 gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, const float* B,
                          int64_t ldb, const float* bias, float* C, int64_t ldc,
                          const int32_t* labels, float scale, const float* scale_dev,
@@ -2298,27 +2371,27 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
     GCG_HIP_CHECK(hipGetLastError());
     const auto* wsp = static_cast<const unsigned*>(ws);
     if (wide && tile == 3) {
-      hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 0, 1, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
+      GCG_FUSED6_LAUNCH((4, 2, 1, 8, 0, 1, 1), dim3(static_cast<unsigned>((M + 63) / 64)),
                          dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels,
                          scale, scale_dev, loss_rows, correct_rows, row_w, wsp);
     } else if (wide) {
-      hipLaunchKernelGGL((gemm_fused6_kernel<4, 2, 1, 8, 0, 1>), dim3(static_cast<unsigned>((M + 63) / 64)),
+      GCG_FUSED6_LAUNCH((4, 2, 1, 8, 0, 1, 0), dim3(static_cast<unsigned>((M + 63) / 64)),
                          dim3(512), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels,
                          scale, scale_dev, loss_rows, correct_rows, row_w, wsp);
     } else if (tile == 3) {  // the 32-row form with the cooperative A split
       const dim3 grid(static_cast<unsigned>((M + 31) / 32));
       switch (g) {
-        case 1: hipLaunchKernelGGL((gemm_fused6_kernel<2, 1, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
-        case 2: hipLaunchKernelGGL((gemm_fused6_kernel<2, 2, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
-        default: hipLaunchKernelGGL((gemm_fused6_kernel<2, 3, 1, 4, 0, 1, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 1: GCG_FUSED6_LAUNCH((2, 1, 1, 4, 0, 1, 1), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 2: GCG_FUSED6_LAUNCH((2, 2, 1, 4, 0, 1, 1), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        default: GCG_FUSED6_LAUNCH((2, 3, 1, 4, 0, 1, 1), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
       }
     } else {
       const dim3 grid(static_cast<unsigned>((M + 31) / 32));
       switch (g) {
-        case 1: hipLaunchKernelGGL((gemm_fused6_kernel<2, 1, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
-        case 2: hipLaunchKernelGGL((gemm_fused6_kernel<2, 2, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
-        case 3: hipLaunchKernelGGL((gemm_fused6_kernel<2, 3, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
-        default: hipLaunchKernelGGL((gemm_fused6_kernel<2, 4, 1, 4, 0, 1>), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 1: GCG_FUSED6_LAUNCH((2, 1, 1, 4, 0, 1, 0), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 2: GCG_FUSED6_LAUNCH((2, 2, 1, 4, 0, 1, 0), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        case 3: GCG_FUSED6_LAUNCH((2, 3, 1, 4, 0, 1, 0), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
+        default: GCG_FUSED6_LAUNCH((2, 4, 1, 4, 0, 1, 0), grid, dim3(256), 0, st, int(M), N, K, A, lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows, correct_rows, row_w, wsp); break;
       }
     }
     GCG_HIP_CHECK(hipGetLastError());
@@ -2329,7 +2402,7 @@ gcg_status launch_fused6(int64_t M, int N, int K, const float* A, int64_t lda, c
   const dim3 grid(static_cast<unsigned>((M + 31) / 32));
 #define GCG_FUSED6_CASE(g_)                                                                    \
   if (g == g_) {                                                                              \
-    hipLaunchKernelGGL((gemm_fused6_kernel<2, g_, 1>), grid, dim3(256), 0, st, int(M), N, K, A, \
+    GCG_FUSED6_LAUNCH((2, g_, 1, 4, 0, 0, 0), grid, dim3(256), 0, st, int(M), N, K, A, \
                        lda, B, ldb, bias, C, ldc, labels, scale, scale_dev, loss_rows,        \
                        correct_rows, row_w);                                                  \
     GCG_HIP_CHECK(hipGetLastError());                                                         \
@@ -2438,9 +2511,15 @@ gcg_status launch_nt3_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
-  hipLaunchKernelGGL((gemm_nt3_kernel<RT, G, WR, WC, S>), dim3(static_cast<unsigned>(rt * ct)),
-                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
-                     a.act, a.C, a.ldc, static_cast<int>(ct));
+  if (a.K - 32 * ((a.K - 1) / 32) <= 16) {  // the last chunk packed (mfma6)
+    hipLaunchKernelGGL((gemm_nt3_kernel<RT, G, WR, WC, S, true>), dim3(static_cast<unsigned>(rt * ct)),
+                       dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                       a.act, a.C, a.ldc, static_cast<int>(ct));
+  } else {
+    hipLaunchKernelGGL((gemm_nt3_kernel<RT, G, WR, WC, S>), dim3(static_cast<unsigned>(rt * ct)),
+                       dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                       a.act, a.C, a.ldc, static_cast<int>(ct));
+  }
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }
@@ -2450,9 +2529,15 @@ gcg_status launch_nt3r_t(const NtArgs& a, const unsigned* Bs, hipStream_t st) {
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
-  hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC, V>), dim3(static_cast<unsigned>(rt * ct)),
-                     dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
-                     a.act, a.C, a.ldc, static_cast<int>(ct));
+  if (a.K - 32 * ((a.K - 1) / 32) <= 16) {  // the last chunk packed (mfma6)
+    hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC, V | 2>), dim3(static_cast<unsigned>(rt * ct)),
+                       dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                       a.act, a.C, a.ldc, static_cast<int>(ct));
+  } else {
+    hipLaunchKernelGGL((gemm_nt3r_kernel<RT, G, WR, WC, V>), dim3(static_cast<unsigned>(rt * ct)),
+                       dim3(64 * WR * WC), 0, st, a.M, a.N, a.K, a.A, a.lda, Bs, a.Bt, a.ldb, a.bias,
+                       a.act, a.C, a.ldc, static_cast<int>(ct));
+  }
   GCG_HIP_CHECK(hipGetLastError());
   return GCG_OK;
 }
@@ -2462,6 +2547,16 @@ gcg_status launch_nt_t(const NtArgs& a, hipStream_t st) {
   constexpr int BM = 16 * RT * WR, BN = 64 * G * WC;
   const int64_t rt = (a.M + BM - 1) / BM, ct = (a.N + BN - 1) / BN;
   if (rt * ct > 0x7fffffffLL) return fail(GCG_ERR_INVALID_ARG, "gemm_nt: M too large");
+  if constexpr (MX == 1) {
+    if (a.K - 32 * ((a.K - 1) / 32) <= 16) {  // the last chunk packed (mfma6)
+      hipLaunchKernelGGL((gemm_nt_kernel<RT, G, WR, WC, S, PF, KC, MX | 2>),
+                         dim3(static_cast<unsigned>(rt * ct)), dim3(64 * WR * WC), 0, st, a.M, a.N,
+                         a.K, a.A, a.lda, a.Bt, a.ldb, a.bias, a.act, a.C, a.ldc,
+                         static_cast<int>(ct));
+      GCG_HIP_CHECK(hipGetLastError());
+      return GCG_OK;
+    }
+  }
   hipLaunchKernelGGL((gemm_nt_kernel<RT, G, WR, WC, S, PF, KC, MX>),
                      dim3(static_cast<unsigned>(rt * ct)), dim3(64 * WR * WC), 0, st, a.M, a.N,
                      a.K, a.A, a.lda, a.Bt, a.ldb, a.bias, a.act, a.C, a.ldc,

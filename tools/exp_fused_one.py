@@ -1,6 +1,7 @@
 #!/usr/bin/env python
 """Fused output layer timing (Twitter-World 840k x 300 x 930 and Twitter-US 270k x 300 x 256),
-every (math, tile) of gcg_project_softmax_xent, outputs checked against float64 on sampled rows."""
+every (math, tile) of gcg_project_softmax_xent, outputs checked against float64 on sampled rows.
+`--bf16x6`: the bf16x6 tiles only; `--rounds R`: time every form R times, alternating."""
 import json
 import os
 import sys
@@ -13,6 +14,8 @@ from graphconvgeo_amd import dense  # noqa: E402
 from graphconvgeo_amd.sparse import empty_dense  # noqa: E402
 from oracle import gcn_oracle as O  # noqa: E402
 
+BF_ONLY = "--bf16x6" in sys.argv
+ROUNDS = int(sys.argv[sys.argv.index("--rounds") + 1]) if "--rounds" in sys.argv else 1
 dev = torch.device("cuda:0")
 g = torch.Generator(device=dev).manual_seed(0)
 for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
@@ -29,8 +32,9 @@ for T, K, C in ((840_000, 300, 930), (270_000, 300, 256)):
     logits64 = P[rows].double() @ W.double() + b.double()
     _, l64, h64, G64 = O.softmax_xent_f64(logits64.cpu().numpy(), y[rows].cpu().numpy(), scale=1.0 / T)
     s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    forms = [("bf16x6", t) for t in (range(4) if C > 768 else (0, 1, 3))] + [("f32", t) for t in range(6)]
-    for math, tile in forms:
+    forms = [("bf16x6", t) for t in ((0, 1, 2, 3) if C > 768 else (0, 1, 3))]
+    forms += [] if BF_ONLY else [("f32", t) for t in range(6)]
+    for math, tile in [f for _ in range(ROUNDS) for f in forms]:
       f = lambda: dense._fused(P, Wp, b, y, 1.0 / T, None, G, loss, hits, math=math, tile=tile)  # noqa: E731
       f()
       torch.cuda.synchronize()
