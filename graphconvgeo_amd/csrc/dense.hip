@@ -2704,8 +2704,31 @@ gcg_status gemm_nt_impl(const char* fn, int64_t M, int64_t N, int64_t K, const f
   hipLaunchKernelGGL(split3_rows_kernel, dim3(static_cast<unsigned>((threads + 255) / 256)), dim3(256),
                      0, st, int(N), int(K), Kc, Bt, ldbt, static_cast<unsigned*>(ws));
   GCG_HIP_CHECK(hipGetLastError());
-  return launch_nt3(tile == 0 ? pick_nt3_shape(N, K) : kNt3Tiles[tile - 1], st, a,
-                    static_cast<const unsigned*>(ws));
+  const auto* wsp = static_cast<const unsigned*>(ws);
+  if (tile == 0) {
+    // Ragged column split (round 6): the 192-column tile over N's whole 192-column blocks and
+    // the narrowest tile over the rest, when that pads less than the one shape the picker
+    // chose. dP = G.W2^T at N = 300, K = 930: the picker's 128 x 192 tile (two passes over A)
+    // computes 384 columns; 192 + 128 computes 320, with the same two passes over A. Every
+    // output element is the same products in the same order (bitwise the one-shape result).
+    const Nt3Shape sh = pick_nt3_shape(N, K);
+    const int64_t bn = 64 * sh.G, pad_pick = (N + bn - 1) / bn * bn;
+    const int64_t n_main = N / 192 * 192, r = N - n_main, gr = (r + 63) / 64;
+    if (n_main > 0 && r > 0 && n_main + 64 * gr < pad_pick) {
+      NtArgs a1 = a;
+      a1.N = static_cast<int>(n_main);
+      gcg_status s1 = launch_nt3(Nt3Shape{2, 3, 4, 1, 1}, st, a1, wsp);
+      if (s1 != GCG_OK) return s1;
+      NtArgs a2 = a;  // columns n_main .. N - 1: their weight rows, planes, bias and outputs
+      a2.N = static_cast<int>(r);
+      a2.Bt = Bt + n_main * ldbt;
+      a2.bias = bias != nullptr ? bias + n_main : nullptr;
+      a2.C = C + n_main;
+      return launch_nt3(Nt3Shape{2, static_cast<int>(gr), 4, 1, gr == 3 ? 1 : 0}, st, a2,
+                        wsp + n_main * Kc * 48);
+    }
+  }
+  return launch_nt3(tile == 0 ? pick_nt3_shape(N, K) : kNt3Tiles[tile - 1], st, a, wsp);
 }
 
 gcg_status gemm_tn_impl(const char* fn, int64_t R, int64_t M, int64_t N, const float* A,
