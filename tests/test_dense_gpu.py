@@ -207,7 +207,8 @@ def test_fused_split_pingpong_bitwise(cuda, M, K, N):
 
 
 @pytest.mark.parametrize("M,K,N", [(37, 16, 129), (513, 300, 930), (70, 33, 1024), (65, 17, 600),
-                                   (9, 4, 61), (5, 7, 801), (128, 64, 1021)])
+                                   (9, 4, 61), (5, 7, 801), (128, 64, 1021), (100, 48, 930),
+                                   (100, 49, 930)])
 def test_fused6_row_bands_bitwise(cuda, M, K, N, monkeypatch):
     """gemm_fused6_kernel's forms (math GCG_MATH_BF16X6): the weight split in every workgroup's
     registers (no workspace; dense.FUSED_PRESPLIT off), the weight's planes pre-split into the
@@ -430,12 +431,15 @@ def test_gemm_nt_tile_variants(cuda, tile):
 
 
 @pytest.mark.parametrize("M,K,N", [(333, 301, 133), (1000, 300, 930), (517, 930, 300),
-                                   (70, 33, 65), (1, 5, 3)])
+                                   (70, 33, 65), (1, 5, 3), (130, 48, 77), (131, 49, 77),
+                                   (300, 600, 600)])
 def test_gemm_nt_bf16x6_tiles_bitwise(cuda, M, K, N):
     """Every bf16x6 tile (gcg_gemm_nt math GCG_MATH_BF16X6, tiles 0..9: A in registers or through
     LDS, the weight planes read from LDS one slot ahead or not) and the in-loop split of both operands accumulate the same six plane products in the
     same order: bitwise equal to each other, with bias + relu, ragged M / N / K; within the
-    float64 bar."""
+    float64 bar. The K tail is packed (mfma6) when the last chunk holds <= 16 k (K = 48: 16,
+    K = 49: 17 -- not packed); tile 0 at K > 512 splits N ragged where that pads less (N = 300:
+    192 + 128 columns; N = 600: 576 + 64)."""
     assert dense.tile_count("gemm_nt", "bf16x6") == 9
     A, B, b = _rand((M, K), 13), _rand((K, N), 14), _rand((N,), 15)
     At, Bt = torch.from_numpy(A).to(cuda), _padded(B, cuda, transpose=True)
