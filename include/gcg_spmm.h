@@ -366,7 +366,10 @@ gcg_status gcg_project_mention_graph(int64_t n_targets, int64_t n_nodes, int64_t
  *                          dropped a1b2 + a2b1 + a2b2 are <= (2^-24 + 2^-34) |a||b| per product --
  *                          one f32 rounding of the product (tests/test_bf16x6_numerics.py pins
  *                          these bounds; tests/test_dense_gpu.py the whole product's error against
- *                          float64, <= 1.25 x the f32 kernel's).
+ *                          float64, <= 1.25 x the f32 kernel's). A last k chunk with <= 16 live
+ *                          k carries two plane products per MFMA (the fragments' zero high halves
+ *                          hold another plane of the low halves' k): 3 MFMAs instead of 6 there,
+ *                          every product still exact, the same in every bf16x6 form.
  *                          f32 semantics at the edges: a tile whose bf16x6 result is not finite
  *                          (an infinite operand, |x| above bf16's largest finite 3.39e38, NaN, or
  *                          overflow) is recomputed on the f32 MFMA in the f32 kernel's k order, so
@@ -404,9 +407,11 @@ gcg_status gcg_gemm_f32(int64_t M, int64_t N, int64_t K, const float* A, int64_t
  *     k chunks (tile 0: 16-deep chunks, 4 stages); every tile the same k order.
  *   GCG_MATH_BF16X6: ws != NULL (gcg_gemm_nt_workspace(N, K, math) bytes, 16-B aligned): Bt's
  *     three planes split once per call into it by a small kernel on the same stream, A split in
- *     registers (tile 0: A in registers, 128 x 64 G columns with G padding N least); ws == NULL:
- *     both operands split in the loop (tile 0 only). Every bf16x6 form accumulates the same six
- *     plane products in the same order: bitwise equal to each other.
+ *     registers (tile 0: A in registers, 128 x 64 G columns with G padding N least, or -- where
+ *     that pads less -- 128 x 192 tiles over N's whole 192-column blocks and the narrowest tile
+ *     over the rest, as two launches on the stream); ws == NULL: both operands split in the loop
+ *     (tile 0 only). Every bf16x6 form accumulates the same six plane products in the same order:
+ *     bitwise equal to each other.
  * gcg_gemm_nt_f32 = gcg_gemm_nt(..., GCG_MATH_F32, 0, NULL, 0, ...);
  * gcg_gemm_nt_f32_bf16x6 = gcg_gemm_nt(..., GCG_MATH_BF16X6, 0, ws, ws_bytes, ...).
  */
