@@ -264,10 +264,14 @@ _SIDE_STREAMS: dict = {}
 SIDE_STREAM_WEIGHT_GRADS = True
 
 
+# priority of the side stream (torch: lower = higher priority; 0 = the default's)
+SIDE_STREAM_PRIORITY = 0
+
+
 def _side_stream(device) -> torch.cuda.Stream:
     s = _SIDE_STREAMS.get(device)
     if s is None:
-        s = torch.cuda.Stream(device=device)
+        s = torch.cuda.Stream(device=device, priority=SIDE_STREAM_PRIORITY)
         _SIDE_STREAMS[device] = s
     return s
 

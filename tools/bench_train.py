@@ -47,6 +47,8 @@ def main():
                     help="weight gradients on the main stream (dense.SIDE_STREAM_WEIGHT_GRADS off)")
     ap.add_argument("--inline-head", action="store_true",
                     help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
+    ap.add_argument("--side-priority", type=int, default=None,
+                    help="priority of the side stream (dense.SIDE_STREAM_PRIORITY; -1 = high)")
     ap.add_argument("--theano-backward", action="store_true",
                     help="reference order: autograd in Theano's association "
                          "(layers.REASSOCIATED_BACKWARD off)")
@@ -58,6 +60,8 @@ def main():
     from graphconvgeo_amd import dense
     if args.nt_math:
         dense.NT_MATH = args.nt_math
+    if args.side_priority is not None:
+        dense.SIDE_STREAM_PRIORITY = args.side_priority
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
     if args.inline_weight_grads:
@@ -115,7 +119,7 @@ def main():
            "mode": args.mode, "order": f"{args.order} -> {clf.l_out.order}", "hip_graph": args.graph,
            "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
            "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
-           "theano_backward": args.theano_backward,
+           "theano_backward": args.theano_backward, "side_priority": dense.SIDE_STREAM_PRIORITY,
            "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
