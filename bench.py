@@ -434,7 +434,8 @@ def dense_kernels_bench(reps: int, dev) -> dict:
         "gemm_nt: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP, math="bf16x6"),
         "gemm_nt f32 MFMA: P.W2 + b2": lambda: dense.gemm_nt(P, W_ck, bias=b, out=G, math="f32"),
         "gemm_nt f32 MFMA: dP = G.W2^T": lambda: dense.gemm_nt(G, W_kc, out=dP, math="f32"),
-        "gemm_tn: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G),
+        "gemm_tn: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G, math="bf16x6"),
+        "gemm_tn f32 MFMA: dW2 = P^T.G (split-K)": lambda: dense.gemm_tn(P, G, math="f32"),
         "fused: P.W2 + b2 -> softmax-CE, hits, dlogits (mlpconv.py:88-95)":
             lambda: dense._fused(P, W_kc, b, y, 1.0 / T, None, G, loss, hits, math="bf16x6"),
         "fused f32 MFMA: P.W2 + b2 -> softmax-CE, hits, dlogits":
@@ -445,7 +446,7 @@ def dense_kernels_bench(reps: int, dev) -> dict:
     out = {"shape": f"{T} x {K} x {C}", "peak_TFLOPs": MFMA_F32_PEAK_TFLOPS,
            "bf16_peak_TFLOPs": MFMA_BF16_PEAK_TFLOPS,
            "note": "TFLOPs = useful f32 FLOP/s; frac against the f32 MFMA peak. gemm_nt (the "
-                   "default, dense.NT_MATH) and the fused layer run bf16x6: six bf16 plane products per f32 "
+                   "default, dense.NT_MATH), gemm_tn (dense.TN_MATH) and the fused layer run bf16x6: six bf16 plane products per f32 "
                    "product on the bf16 matrix cores (error vs float64 <= the f32 kernel's, "
                    "tests/test_dense_gpu.py); the bf16x6 forms split the weight's planes into a "
                    "workspace first, that launch inside the timed call; its frac = 6 x FLOP/s / the bf16 peak, "
@@ -457,7 +458,7 @@ def dense_kernels_bench(reps: int, dev) -> dict:
         tf = flops / (ms * 1e-3) / 1e12
         out[name] = {"ms": round(ms, 3), "TFLOPs": round(tf, 1),
                      "frac": round(tf / MFMA_F32_PEAK_TFLOPS, 3)}
-        if name.startswith(("gemm_nt:", "fused:")):  # bf16x6: the bf16 pipe, 6 MFMA FLOP per FLOP
+        if name.startswith(("gemm_nt:", "gemm_tn:", "fused:")):  # bf16x6: the bf16 pipe, 6 MFMA FLOP per FLOP
             out[name].update(math="bf16x6", frac=round(6 * tf / MFMA_BF16_PEAK_TFLOPS, 3),
                              f32_equivalent_frac=round(tf / MFMA_F32_PEAK_TFLOPS, 3))
     del P, G, dP, W_kc, W_ck

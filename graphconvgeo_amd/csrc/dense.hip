@@ -2088,6 +2088,127 @@ __global__ __launch_bounds__(WM <= 1 ? 256 : 64 * WM, (WM == 0 && OCC != 2) ? 1 
       }
 }
 
+// gemm_tn6_partial_kernel (round 6): gemm_tn_partial_kernel's split-K A^T . B (the weight
+// gradients dW2 = P^T . G and X_head^T . G) on the bf16 matrix cores (bf16x6, mfma6). Each wave
+// owns a 64 (m) x 64 (n) tile of one split: per 32-row chunk, lane (j, q) loads rows
+// t0 + 4q + i and t0 + 16 + 4q + i (i < 4) of A and B as dwordx4 of 4 adjacent columns (the
+// fused layer's in-register weight load), which gives, for each of its 4 column slots e
+// (column m0 + 4j + e), the 8 k-values of its MFMA fragment in the bf16x6 kernels' k order;
+// the fragments are split into planes in registers. The D row rho of block (eA, eB) is
+// m = m0 + 4 rho + eA, its column j is n = n0 + 4j + eB, so each lane stores 4 adjacent n of
+// 16 rows. Rows past the split come from a buffer range that reads 0; columns past M / N are
+// computed on a clamped column and never reach C (the reduce kernel reads m < M, n < N). A tile
+// whose accumulators are not finite is recomputed with f32 products (v_mfma_f32_16x16x4_f32,
+// one row t per k step) -- f32 semantics, as the other bf16x6 kernels.
+__global__ __launch_bounds__(256, 2) void gemm_tn6_partial_kernel(
+    int R, int M, int N, const float* __restrict__ A, int64_t lda, const float* __restrict__ B,
+    int64_t ldb, int rows_per_split, float* __restrict__ part, int Mp, int Np, int mt, int nt) {
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int j = lane & 15, q = lane >> 4;
+  const int nwg = static_cast<int>(gridDim.x), b = static_cast<int>(blockIdx.x);
+  const int xcd = b % 8, qq = nwg / 8, rr = nwg % 8;  // XCD-aware order, as gemm_tn_partial
+  const int tile = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + b / 8;
+  const int wt = 4 * tile + wave;
+  const int bx = wt % mt, by = (wt / mt) % nt, bz = wt / (mt * nt);
+  const int m0 = bx * 64, n0 = by * 64;
+  if (m0 >= M || n0 >= N) return;  // wave-uniform; no barriers in this kernel
+  if (static_cast<int64_t>(bz) * rows_per_split >= R) return;
+  const int t_begin = bz * rows_per_split;
+  const int rows = min(R, t_begin + rows_per_split) - t_begin;
+  const int m4 = (M + 3) & ~3, n4 = (N + 3) & ~3;
+  const int ac = m0 + 4 * j < m4 ? m0 + 4 * j : 0;
+  const int bc = n0 + 4 * j < n4 ? n0 + 4 * j : 0;
+  const int lda4 = static_cast<int>(lda) * 4, ldb4 = static_cast<int>(ldb) * 4;
+  const float* Ab = A + static_cast<int64_t>(t_begin) * lda;
+  const float* Bb = B + static_cast<int64_t>(t_begin) * ldb;
+  const int aoff = 4 * q * lda4 + ac * 4, boff = 4 * q * ldb4 + bc * 4;
+  const int nch = (rows + 31) / 32;
+  auto load = [&](int c, f4 (&xa)[8], f4 (&xb)[8]) {
+    const int live = min(rows - 32 * c, 32);  // rows of this chunk inside the split
+    const auto ra = brsrc(Ab + static_cast<int64_t>(32 * c) * lda, live * lda4);
+    const auto rb = brsrc(Bb + static_cast<int64_t>(32 * c) * ldb, live * ldb4);
+    // (the row offset in the VGPR offset, which the range check covers: rows past the split
+    // must read 0, they are the next split's)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      xa[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + i * lda4, 0, 0));
+      xa[4 + i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, aoff + (16 + i) * lda4, 0, 0));
+      xb[i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + i * ldb4, 0, 0));
+      xb[4 + i] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, boff + (16 + i) * ldb4, 0, 0));
+    }
+  };
+  f4 acc[4][4];
+#pragma unroll
+  for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+    for (int eb = 0; eb < 4; ++eb) acc[ea][eb] = f4{0.f, 0.f, 0.f, 0.f};
+  f4 xa[8], xb[8], na[8], nb[8];
+  load(0, xa, xb);
+  for (int c = 0; c < nch; ++c) {
+    if (c + 1 < nch) load(c + 1, na, nb);  // one chunk ahead
+    bf8 ap[4][3];
+#pragma unroll
+    for (int ea = 0; ea < 4; ++ea) {
+      const f8 y = {xa[0][ea], xa[1][ea], xa[2][ea], xa[3][ea], xa[4][ea], xa[5][ea], xa[6][ea], xa[7][ea]};
+      split3(y, ap[ea][0], ap[ea][1], ap[ea][2]);
+    }
+#pragma unroll
+    for (int eb = 0; eb < 4; ++eb) {
+      const f8 y = {xb[0][eb], xb[1][eb], xb[2][eb], xb[3][eb], xb[4][eb], xb[5][eb], xb[6][eb], xb[7][eb]};
+      bf8 b0, b1, b2;
+      split3(y, b0, b1, b2);
+      // the chunk's six plane products into a fresh accumulator, then one f32 add into the
+      // tile's: a split's thousands of rows cost one rounding of the running sum per 32 rows,
+      // not six (accumulated straight into the running sum, World dW2 came out ~3 x less
+      // accurate than the f32 kernel's, whose MFMA adds 4 rows per rounding)
+#pragma unroll
+      for (int ea = 0; ea < 4; ++ea)
+        acc[ea][eb] += mfma6<false>(ap[ea], b0, b1, b2, f4{0.f, 0.f, 0.f, 0.f});
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      xa[i] = na[i];
+      xb[i] = nb[i];
+    }
+  }
+  // f32 semantics for Inf / huge operands (x * 0 is NaN only for a non-finite x)
+  f2 sn = {0.f, 0.f};
+#pragma unroll
+  for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+    for (int eb = 0; eb < 4; ++eb) {
+      sn = __builtin_elementwise_fma(f2{acc[ea][eb][0], acc[ea][eb][1]}, f2{0.f, 0.f}, sn);
+      sn = __builtin_elementwise_fma(f2{acc[ea][eb][2], acc[ea][eb][3]}, f2{0.f, 0.f}, sn);
+    }
+  if (__builtin_amdgcn_ballot_w64(sn[0] != sn[0] || sn[1] != sn[1]) != 0) {
+#pragma unroll
+    for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+      for (int eb = 0; eb < 4; ++eb) acc[ea][eb] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < rows; t += 4) {  // k step: row t + q
+      const int live = min(rows - t, 4);
+      const auto ra = brsrc(Ab + static_cast<int64_t>(t) * lda, live * lda4);
+      const auto rb = brsrc(Bb + static_cast<int64_t>(t) * ldb, live * ldb4);
+      const f4 a = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(ra, q * lda4 + ac * 4, 0, 0));
+      const f4 bv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(rb, q * ldb4 + bc * 4, 0, 0));
+#pragma unroll
+      for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+        for (int eb = 0; eb < 4; ++eb) acc[ea][eb] = mfma4(a[ea], bv[eb], acc[ea][eb]);
+    }
+  }
+  float* pt = part + static_cast<int64_t>(bz) * Mp * Np;
+#pragma unroll
+  for (int ea = 0; ea < 4; ++ea)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = m0 + 4 * (4 * q + r) + ea;
+      const f4 o = {acc[ea][0][r], acc[ea][1][r], acc[ea][2][r], acc[ea][3][r]};
+      *reinterpret_cast<f4*>(pt + static_cast<int64_t>(m) * Np + n0 + 4 * j) = o;
+    }
+}
+
 // C[m][n] = scale * sum over the S split partials part[s][m][n], deterministic. One workgroup
 // per (row m, 64 column quads): wave w of the 8 sums the splits s = w, w + 8, ... (4 loads in
 // flight per lane), then the 8 wave sums are added in wave order through LDS. (One thread per
@@ -2156,7 +2277,7 @@ constexpr int kTnTiles[][5] = {
 };
 constexpr int kTnTileCount = sizeof(kTnTiles) / sizeof(kTnTiles[0]);
 
-TnPlan tn_plan(int64_t R, int64_t M, int64_t N, int tile = 0) {
+TnPlan tn_plan(int64_t R, int64_t M, int64_t N, int tile = 0, bool bf16x6 = false) {
   TnPlan p;
   // Default: per-wave 64 x 64*NG tiles (WM = 0), NG = 3 or 2, whichever pads N less (ties: 3,
   // fewer loads per MFMA). The round-2 workgroup tiles (WM = 1: 4 waves side by side, 64 x
@@ -2185,6 +2306,7 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N, int tile = 0) {
     const int* t = kTnTiles[tile - 1];
     p.mg = t[0], p.ng = t[1], p.pd = t[2], p.wm = t[3], p.occ = t[4], slots = 2048;
   }
+  if (bf16x6) p.mg = 1, p.ng = 1, p.pd = 0, p.wm = 0, p.occ = 0, slots = 8192;  // gemm_tn6
   const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
   const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
   p.mt = static_cast<int>((M + tm - 1) / tm);
@@ -2752,7 +2874,8 @@ gcg_status gemm_tn_impl(const char* fn, int64_t R, int64_t M, int64_t N, const f
       GCG_HIP_CHECK(hipMemsetAsync(C + m * ldc, 0, sizeof(float) * N, s));
     return GCG_OK;
   }
-  const TnPlan p = tn_plan(R, M, N, tile);
+  const bool bf = math == GCG_MATH_BF16X6;
+  const TnPlan p = tn_plan(R, M, N, tile, bf);
   const size_t need = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
   if (workspace == nullptr || workspace_bytes < need)
     return fail(GCG_ERR_WORKSPACE, "%s: workspace %zu bytes < %zu needed", fn, workspace_bytes,
@@ -2764,6 +2887,10 @@ gcg_status gemm_tn_impl(const char* fn, int64_t R, int64_t M, int64_t N, const f
   if (p.wm == 0) n_tiles = (n_tiles + 3) / 4;  // 4 wave tiles per workgroup
   const dim3 grid(static_cast<unsigned>(n_tiles));
   constexpr int remap = 1;  // XCD-aware tile order (+1-3 % dW2, +14 % X head)
+  if (bf) {
+    hipLaunchKernelGGL(gemm_tn6_partial_kernel, grid, dim3(256), 0, s, int(R), int(M), int(N), A,
+                       lda, B, ldb, p.rows_per_split, part, p.Mp, p.Np, p.mt, p.nt);
+  } else
 #define GCG_TN_CASE_OCC(MG_, NG_, PD_, WM_, OCC_)                                            \
   if (p.mg == MG_ && p.ng == NG_ && p.pd == PD_ && p.wm == WM_ && p.occ == OCC_) {           \
     hipLaunchKernelGGL((gemm_tn_partial_kernel<MG_, NG_, PD_, WM_, OCC_>), grid,             \
@@ -2806,7 +2933,8 @@ int32_t gcg_dense_tile_count(int32_t op, int32_t math) {
       return math == GCG_MATH_F32 ? kNtTileCount : math == GCG_MATH_BF16X6 ? kNt3TileCount : -1;
     case GCG_DENSE_FUSED:
       return math == GCG_MATH_F32 ? 5 : math == GCG_MATH_BF16X6 ? 3 : -1;
-    case GCG_DENSE_GEMM_TN: return math == GCG_MATH_F32 ? kTnTileCount : -1;
+    case GCG_DENSE_GEMM_TN:
+      return math == GCG_MATH_F32 ? kTnTileCount : math == GCG_MATH_BF16X6 ? 0 : -1;
     default: return -1;
   }
 }
@@ -2978,7 +3106,7 @@ gcg_status gcg_gemm_tn_workspace_bytes(int64_t R, int64_t M, int64_t N, int32_t 
       bytes == nullptr)
     return fail(GCG_ERR_INVALID_ARG, "%s: bad sizes", fn);
   if (R == 0) { *bytes = 0; return GCG_OK; }
-  const TnPlan p = tn_plan(R, M, N, tile);
+  const TnPlan p = tn_plan(R, M, N, tile, math == GCG_MATH_BF16X6);
   *bytes = sizeof(float) * static_cast<size_t>(p.S) * p.Mp * p.Np;
   return GCG_OK;
 }

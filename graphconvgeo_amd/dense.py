@@ -17,7 +17,8 @@ Here every product runs in libgcg_spmm.so's MFMA kernels (csrc/dense.hip):
   softmax_xent(logits, y)         loss, acc of logits that already exist (reference order)
   softmax(logits)                 predict_proba
   gemm_tn(A, B)                   C = A^T . B, the weight gradient h^T . g: a split-K MFMA kernel
-                                  (reduction over ~10^6 rows), deterministic
+                                  (reduction over ~10^6 rows; bf16x6 by default, TN_MATH),
+                                  deterministic
 No product of the layer path goes to hipBLASLt / rocBLAS. There is no CPU path: CPU tensors
 raise. Round 4: gemm_nt (NT_MATH) and the fused layer (FUSED_MATH) run their products on the
 bf16 matrix cores at f32 accuracy -- every f32 operand split into three bf16 planes, the six
@@ -210,11 +211,23 @@ def gemm_nt(A: torch.Tensor, Bt: torch.Tensor, bias: Optional[torch.Tensor] = No
 _TN_WS: dict = {}
 
 
+# products of gemm_tn (the weight gradients): "f32" or "bf16x6" (round 6, gemm_tn6_partial_kernel:
+# World dW2 840k x 300 x 930 124.7-126.9 -> 140.6-143.5 TFLOP/s, the X-head gradient 1.4M x 256 x
+# 300 104-111 -> 139, Twitter-US dW2 98-108 -> 119-126, each closer to float64 than the f32
+# kernel: tools/exp_tn_math.py, profiles/r06/tn_math_ab.jsonl)
+TN_MATH = "bf16x6"
+
+
 def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = None,
-            out: Optional[torch.Tensor] = None, tile: int = 0) -> torch.Tensor:
-    """C = scale * A^T . B (the weight gradient h^T . g) on the split-K MFMA kernel (gcg_gemm_tn,
-    f32); deterministic (partials summed in a fixed order). scale: optional device scalar.
-    tile: 0 = the default layout for the shape, 1..tile_count("gemm_tn") another one."""
+            out: Optional[torch.Tensor] = None, tile: int = 0, math: Optional[str] = None
+            ) -> torch.Tensor:
+    """C = scale * A^T . B (the weight gradient h^T . g) on the split-K MFMA kernel (gcg_gemm_tn);
+    deterministic (partials summed in a fixed order). scale: optional device scalar.
+    math: "f32" (f32 MFMA) or "bf16x6" (the bf16 matrix cores, f32-accurate; tile 0 only);
+    None = TN_MATH at tile 0, f32 at another tile. tile: 0 = the default layout for the shape, 1..tile_count("gemm_tn") another
+    one (f32)."""
+    if math is None:  # (the alternative tiles are f32 layouts)
+        math = "f32" if tile else TN_MATH
     A = _aligned_operand(A, "A")
     B = _aligned_operand(B, "B")
     R, M = A.shape
@@ -234,7 +247,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
     if R == 0:
         return out.zero_()
     nb = C.c_size_t()
-    call("gcg_gemm_tn_workspace_bytes", R, M, N, MATHS["f32"], int(tile), C.byref(nb))
+    call("gcg_gemm_tn_workspace_bytes", R, M, N, _math_code(math), int(tile), C.byref(nb))
     key = (A.device, torch.cuda.current_stream(A.device).cuda_stream)
     ws = _TN_WS.get(key)
     if ws is None or ws.numel() * 4 < nb.value:
@@ -244,7 +257,7 @@ def gemm_tn(A: torch.Tensor, B: torch.Tensor, scale: Optional[torch.Tensor] = No
         scale = scale.reshape(1).to(torch.float32).contiguous()
     with torch.cuda.device(A.device):
         call("gcg_gemm_tn", R, M, N, _ptr(A), _ld(A), _ptr(B), _ld(B), _ptr(scale),
-             _ptr(out), out.stride(0) if M > 1 else N, MATHS["f32"], int(tile), _ptr(ws),
+             _ptr(out), out.stride(0) if M > 1 else N, _math_code(math), int(tile), _ptr(ws),
              ws.numel() * 4, _stream_handle(A.device))
     return out
 

@@ -529,13 +529,17 @@ gcg_status gcg_softmax_xent_weighted_f32(int64_t M, int64_t N, const float* logi
 /*
  * Weight gradient C = scale * A^T . B (Theano's grad of T.dot(h, W) w.r.t. W: h^T . gz,
  * mlpconv.py:88; P^T . G in the propagate-first order), A: R x M, B: R x N, C: M x N, the
- * reduction over R (~10^6 rows) split across waves on the f32 MFMA; the per-split partials
- * (caller-owned workspace, size from gcg_gemm_tn_workspace_bytes for the same math and tile) are
- * summed in split order, so the result is deterministic (equal to a BLAS sgemm within f32
- * rounding). A and B: 16-B aligned, lda >= round4(M), ldb >= round4(N), ld % 4 == 0. scale_dev:
- * nullable device scalar. GCG_MATH_F32 only; tile 0 = per-wave 64 x 64 NG tiles (NG padding N
- * least) or, for M <= 256 in 64-row bands with N <= 512, waves stacked along M; tiles 1..7 =
- * other wave layouts and split counts (another summation order: within f32 rounding).
+ * reduction over R (~10^6 rows) split across waves; the per-split partials (caller-owned
+ * workspace, size from gcg_gemm_tn_workspace_bytes for the same math and tile) are summed in
+ * split order, so the result is deterministic (equal to a BLAS sgemm within f32 rounding). A and
+ * B: 16-B aligned, lda >= round4(M), ldb >= round4(N), ld % 4 == 0. scale_dev: nullable device
+ * scalar.
+ *   GCG_MATH_F32 (f32 MFMA): tile 0 = per-wave 64 x 64 NG tiles (NG padding N least) or, for
+ *     M <= 256 in 64-row bands with N <= 512, waves stacked along M; tiles 1..7 = other wave
+ *     layouts and split counts (another summation order: within f32 rounding).
+ *   GCG_MATH_BF16X6 (tile 0 only): per-wave 64 x 64 tiles on the bf16 matrix cores, each
+ *     32-row chunk's six plane products summed apart and added to the split's running sum once
+ *     (error against float64 at or below the f32 form's); non-finite tiles recomputed in f32.
  * gcg_gemm_tn_f32[_workspace_bytes] = the GCG_MATH_F32, tile 0 forms.
  */
 gcg_status gcg_gemm_tn_workspace_bytes(int64_t R, int64_t M, int64_t N, int32_t math,

@@ -55,8 +55,8 @@ def test_bench_single_gpu_line(cuda):
         assert rec["variants"]["fast"]["mode"] == "fast" and rec["variants"]["fast"]["kernel_ms"] > 0
     assert "mode_resolution" in rec["config"]
     dk = {k: v for k, v in rec["dense_kernels"].items() if isinstance(v, dict)}
-    assert len(dk) == 7 and all(v["TFLOPs"] > 0 and v["frac"] < 1 for v in dk.values())
-    assert sum(v.get("math") == "bf16x6" for v in dk.values()) == 3
+    assert len(dk) == 8 and all(v["TFLOPs"] > 0 and v["frac"] < 1 for v in dk.values())
+    assert sum(v.get("math") == "bf16x6" for v in dk.values()) == 4  # NT x 2, TN, fused
 
 
 def test_bench_two_ranks_gloo(cuda):

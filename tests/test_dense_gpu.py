@@ -333,7 +333,7 @@ def test_gemm_tn_layouts_vs_float64(cuda, R, M, N, tile):
     WM = 0 -- the default family -- and waves stacked along M) against float64, with ragged R
     (steps that end inside a split read zeros through the buffer range check), M and N off the
     tiles."""
-    assert dense.tile_count("gemm_tn") == 7 and dense.tile_count("gemm_tn", "bf16x6") == -1
+    assert dense.tile_count("gemm_tn") == 7 and dense.tile_count("gemm_tn", "bf16x6") == 0
     A, B = _rand((R, M), 45, 0.5), _rand((R, N), 46, 0.5)
     At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
     C = dense.gemm_tn(At, Bt, tile=tile).cpu().numpy()
@@ -685,3 +685,47 @@ def test_fused_bf16x6_nonfinite_has_f32_semantics(cuda, N):
     assert fin.sum() == M - len(special)
     assert np.abs(lb[fin] - lf[fin]).max() < 1e-5
     assert np.abs(Gb[fin] - Gf[fin]).max() < 1e-6
+
+
+@pytest.mark.parametrize("R,M,N", [(1000, 300, 930), (4097, 300, 256), (77, 64, 300), (33, 5, 7),
+                                   (513, 256, 300), (20000, 300, 930), (64, 301, 129)])
+def test_gemm_tn_bf16x6_vs_float64(cuda, R, M, N):
+    """gcg_gemm_tn math GCG_MATH_BF16X6 (gemm_tn6_partial_kernel): the split-K weight gradient
+    on the bf16 matrix cores -- error against float64 at most 1.25 x the f32 kernel's (and below
+    2^-20 of sum |a||b|), ragged R / M / N (partial 32-row chunks inside a split: rows past a
+    split must read 0, they belong to the next), deterministic."""
+    rng = np.random.default_rng(R + M + N)
+    A = (rng.choice([-1.0, 1.0], (R, M)) * 10.0 ** rng.uniform(-2, 2, (R, M))).astype(np.float32)
+    B = (rng.choice([-1.0, 1.0], (R, N)) * 10.0 ** rng.uniform(-2, 2, (R, N))).astype(np.float32)
+    At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
+    C64 = A.astype(np.float64).T @ B.astype(np.float64)
+    scale = np.abs(A).astype(np.float64).T @ np.abs(B).astype(np.float64) + 1e-30
+    rel = {}
+    for math in ("f32", "bf16x6"):
+        C = dense.gemm_tn(At, Bt, math=math).cpu().numpy()
+        assert np.array_equal(C, dense.gemm_tn(At, Bt, math=math).cpu().numpy())  # deterministic
+        rel[math] = float((np.abs(C.astype(np.float64) - C64) / scale).max())
+    assert rel["bf16x6"] <= 1.25 * rel["f32"] + 2.0 ** -24 and rel["bf16x6"] < 2.0 ** -20, rel
+
+
+def test_gemm_tn_bf16x6_nonfinite_has_f32_semantics(cuda):
+    """A tile of the bf16x6 TN kernel whose sums are not finite is recomputed with f32 products:
+    Inf propagates with its sign, Inf * 0 and NaN give NaN -- the f32 kernel's NaN / Inf pattern;
+    every other element within the float64 bar."""
+    R, M, N = 300, 70, 90
+    A, B = _rand((R, M), 91), _rand((R, N), 92)
+    A[5, 3] = np.inf
+    B[7, 11] = np.nan
+    A[9, 40] = 3.39e38 * 1.002  # above bf16's largest finite value
+    At, Bt = torch.from_numpy(A).to(cuda), torch.from_numpy(B).to(cuda)
+    ref = dense.gemm_tn(At, Bt, math="f32").cpu().numpy()
+    C = dense.gemm_tn(At, Bt, math="bf16x6").cpu().numpy()
+    assert np.array_equal(np.isnan(C), np.isnan(ref)) and np.array_equal(np.isinf(C), np.isinf(ref))
+    inf = np.isinf(ref)
+    assert np.array_equal(C[inf], ref[inf])
+    fin = np.isfinite(ref)
+    with np.errstate(all="ignore"):
+        C64 = A.astype(np.float64).T @ B.astype(np.float64)
+        bound = 2e-6 * (np.abs(A).astype(np.float64).T @ np.abs(B).astype(np.float64)) + 1e-30
+    ok = fin & np.isfinite(C64)
+    assert (np.abs(C[ok] - C64[ok]) <= bound[ok]).all()
