@@ -2306,7 +2306,10 @@ TnPlan tn_plan(int64_t R, int64_t M, int64_t N, int tile = 0, bool bf16x6 = fals
     const int* t = kTnTiles[tile - 1];
     p.mg = t[0], p.ng = t[1], p.pd = t[2], p.wm = t[3], p.occ = t[4], slots = 2048;
   }
-  if (bf16x6) p.mg = 1, p.ng = 1, p.pd = 0, p.wm = 0, p.occ = 0, slots = 8192;  // gemm_tn6
+#ifndef GCG_TN6_SLOTS  // wave tiles per launch: 4096 / 8192 / 16384 within noise, 32768 -3 %
+#define GCG_TN6_SLOTS 8192  // (variant libraries, tools/gpu/tn_slots.sh, profiles/r06/tn6_slots_ab.txt)
+#endif
+  if (bf16x6) p.mg = 1, p.ng = 1, p.pd = 0, p.wm = 0, p.occ = 0, slots = GCG_TN6_SLOTS;  // gemm_tn6
   const int tm = 64 * p.mg * std::max(1, p.wm);          // C rows per tile
   const int tn = (p.wm == 1 ? 256 : 64) * p.ng;          // C columns per tile
   p.mt = static_cast<int>((M + tm - 1) / tm);
