@@ -1,7 +1,8 @@
 #!/usr/bin/env python
 """Profiling driver: 3 launches each of the fused output kernel (default tile), the plain
-register-B MFMA GEMM and the LDS-DMA NT GEMM (forward 840k x 300 x 930, input gradient
-840k x 930 x 300) at Twitter-World's output-layer shapes (for rocprofv3 --pmc passes)."""
+register-B MFMA GEMM, the NT GEMM (forward 840k x 300 x 930, input gradient 840k x 930 x 300)
+and the split-K weight gradient at Twitter-World's output-layer shapes (for rocprofv3 --pmc
+passes)."""
 import os
 import sys
 
@@ -31,5 +32,7 @@ for _ in range(3):
 dP = empty_dense(T, K, dev)
 for _ in range(3):
     dense.gemm_nt(G, Wp, out=dP)
+for _ in range(3):  # the weight gradient dW2 = P^T . G (bf16x6 split-K, dense.TN_MATH)
+    dense.gemm_tn(P, G)
 torch.cuda.synchronize()
 print("done")
