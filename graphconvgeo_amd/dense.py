@@ -332,6 +332,39 @@ def _weight_on_side_stream(W: torch.Tensor):
     return Wa, slot
 
 
+class _SideBiasGrad(torch.autograd.Function):
+    """Identity on b; its backward computes scale * colsum(G) from the slot (round 6: the
+    output layer's bias gradient, a 2 GB column pass at Twitter-World, leaves the main stream's
+    critical path and runs beside the input gradient's GEMM)."""
+
+    @staticmethod
+    def forward(ctx, b, slot):
+        ctx.slot = slot
+        return b.view_as(b)
+
+    @staticmethod
+    def backward(ctx, _placeholder):
+        if ctx.slot.args is None:  # the consumer produced no bias gradient
+            return None, None
+        G, scale = ctx.slot.args
+        ctx.slot.args = None
+        side = torch.cuda.current_stream(G.device)
+        for t in (G, scale):  # main-stream memory read on the side stream (as _SideWeightGrad)
+            t.record_stream(side)
+        return _colsum(G).mul_(scale), None
+
+
+def _bias_on_side_stream(b: Optional[torch.Tensor]):
+    """(b', slot): b' aliases b; the gradient reaching b' is computed on the side stream."""
+    if b is None or not (SIDE_STREAM_WEIGHT_GRADS and torch.is_grad_enabled() and b.requires_grad
+                         and b.is_cuda):
+        return b, None
+    slot = _Slot()
+    with torch.cuda.stream(_side_stream(b.device)):
+        ba = _SideBiasGrad.apply(b, slot)
+    return ba, slot
+
+
 def _colsum(X: torch.Tensor) -> torch.Tensor:
     """Bias gradient: deterministic HIP column sum (K <= 1024), else torch's reduction."""
     return column_sum(X) if X.dim() == 2 and X.shape[1] <= 1024 else X.sum(dim=0)
@@ -433,7 +466,8 @@ class Projection:
                    row_weight)
             return loss_rows.sum() / D, correct.sum() / D
         Wa, slot = _weight_on_side_stream(W)
-        return _ProjectXent.apply(P, Wa, b, labels, self, denom, slot, row_weight)
+        ba, bslot = _bias_on_side_stream(b)
+        return _ProjectXent.apply(P, Wa, ba, labels, self, denom, slot, row_weight, bslot)
 
     def probabilities(self, P, W, b) -> torch.Tensor:
         """softmax(P . W + b) rows (predict_proba) in one fused launch."""
@@ -511,7 +545,7 @@ class _ProjectXent(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, P, W, b, labels, proj: Projection, denom: Optional[int] = None, slot=None,
-                row_weight=None):
+                row_weight=None, bslot=None):
         P = _aligned_operand(P, "P")
         M, N = P.shape[0], W.shape[1]
         D = float(max(M if denom is None else denom, 1))  # rows the mean is over (all ranks)
@@ -524,7 +558,9 @@ class _ProjectXent(torch.autograd.Function):
         ctx.save_for_backward(P, W, G)
         ctx.proj = proj
         ctx.slot = slot
+        ctx.bslot = bslot
         ctx.has_b = b is not None
+        ctx.b_shape = b.shape if b is not None else None
         loss = loss_rows.sum() / D
         acc = correct.sum() / D
         ctx.mark_non_differentiable(acc)
@@ -536,7 +572,11 @@ class _ProjectXent(torch.autograd.Function):
         gP = gW = gb = None
         g = g_loss.reshape(())
         if ctx.has_b and ctx.needs_input_grad[2]:
-            gb = _colsum(G).mul_(g)
+            if ctx.bslot is not None:  # on the side stream (_bias_on_side_stream)
+                ctx.bslot.args = (G, g)
+                gb = g.new_empty(()).expand(ctx.b_shape)
+            else:
+                gb = _colsum(G).mul_(g)
         if ctx.needs_input_grad[1]:
             # split-K MFMA, the upstream gradient applied on device; on the side stream when
             # W came through _weight_on_side_stream
@@ -548,7 +588,7 @@ class _ProjectXent(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             # dP = G . (g W)^T on the NT GEMM: Bt = g W, a scaled padded copy of W
             gP = gemm_nt(G, ctx.proj.bwd.get(W, False, scale=g))
-        return gP, gW, gb, None, None, None, None, None
+        return gP, gW, gb, None, None, None, None, None, None
 
 
 def _rows_call(logits, y, scale, scale_dev, out, loss_rows, correct, row_weight=None):
@@ -607,8 +647,9 @@ def project_softmax_xent(P, W, b, labels, proj: Optional[Projection] = None,
     if torch.compiler.is_compiling():  # gcg::project_softmax_xent (ops.py)
         return _ops.project_softmax_xent(P, W, b, labels, denom, _row_weight(row_weight, P.shape[0]))
     Wa, slot = _weight_on_side_stream(W)
-    return _ProjectXent.apply(P, Wa, b, labels, proj or Projection(), denom, slot,
-                              _row_weight(row_weight, P.shape[0]))
+    ba, bslot = _bias_on_side_stream(b)
+    return _ProjectXent.apply(P, Wa, ba, labels, proj or Projection(), denom, slot,
+                              _row_weight(row_weight, P.shape[0]), bslot)
 
 
 def softmax_xent(logits: torch.Tensor, labels: torch.Tensor, denom: Optional[int] = None,
