@@ -77,6 +77,12 @@ HYBRID_MAX_COLS = 256
 HYBRID_MIN_ROWS = 65536
 # the dense-head GEMM of tmatmul runs on a side stream beside the tail gather
 TMATMUL_HEAD_SIDE_STREAM = True
+# its products: f32 (round 6). Alone the bf16x6 form is 30 % faster (1.5 vs 2.0 ms at
+# Twitter-World), but beside the tail gather it is starved of CU slots and outlasts the gather
+# (9.0 ms in the step's kernel trace): World step 39.09-39.11 -> 38.91-38.98 ms, Twitter-US
+# 9.43-9.45 -> 9.35-9.37 with the f32 kernel here (profiles/r06/head_math_ab.txt,
+# tools/gpu/head_math.sh). None: dense.TN_MATH.
+TMATMUL_HEAD_MATH = "f32"
 
 # Gather hint (round 3, DeviceCSR.gather_hint): on a skewed matrix whose dense operand is far
 # larger than the Infinity Cache, the rows of all but the most frequent columns are gathered
@@ -519,7 +525,7 @@ class DeviceCSR:
         side.wait_stream(main)
         with torch.cuda.stream(side):
             G.record_stream(side)  # G (main-stream memory) is read on the side stream
-            head = dense.gemm_tn(Xh, G)
+            head = dense.gemm_tn(Xh, G, math=TMATMUL_HEAD_MATH)
             head.record_stream(main)  # side-stream memory, read by the index_copy below
         out = spmm(tail_t, G, mode=mode, out=out)
         main.wait_stream(side)
