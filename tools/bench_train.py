@@ -47,6 +47,8 @@ def main():
                     help="weight gradients on the main stream (dense.SIDE_STREAM_WEIGHT_GRADS off)")
     ap.add_argument("--inline-head", action="store_true",
                     help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
+    ap.add_argument("--tn-math", default=None, choices=["f32", "bf16x6"],
+                    help="products of the weight gradients (dense.TN_MATH)")
     ap.add_argument("--head-math", default=None, choices=["f32", "bf16x6"],
                     help="products of the X^T.g dense-head GEMM (sparse.TMATMUL_HEAD_MATH)")
     ap.add_argument("--side-priority", type=int, default=None,
@@ -66,6 +68,8 @@ def main():
         dense.SIDE_STREAM_PRIORITY = args.side_priority
     if args.head_math is not None:
         gs.TMATMUL_HEAD_MATH = args.head_math
+    if args.tn_math is not None:
+        dense.TN_MATH = args.tn_math
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
     if args.inline_weight_grads:
@@ -124,7 +128,7 @@ def main():
            "inline_weight_grads": args.inline_weight_grads, "inline_head": args.inline_head,
            "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
            "theano_backward": args.theano_backward, "side_priority": dense.SIDE_STREAM_PRIORITY,
-           "head_math": gs.TMATMUL_HEAD_MATH or dense.TN_MATH,
+           "head_math": gs.TMATMUL_HEAD_MATH or dense.TN_MATH, "tn_math": dense.TN_MATH,
            "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
