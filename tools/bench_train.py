@@ -47,6 +47,8 @@ def main():
                     help="weight gradients on the main stream (dense.SIDE_STREAM_WEIGHT_GRADS off)")
     ap.add_argument("--inline-head", action="store_true",
                     help="X^T.G dense-head GEMM on the main stream (sparse.TMATMUL_HEAD_SIDE_STREAM off)")
+    ap.add_argument("--hybrid-max-cols", type=int, default=None,
+                    help="dense-head columns of X^T.g at most (sparse.HYBRID_MAX_COLS)")
     ap.add_argument("--tn-math", default=None, choices=["f32", "bf16x6"],
                     help="products of the weight gradients (dense.TN_MATH)")
     ap.add_argument("--head-math", default=None, choices=["f32", "bf16x6"],
@@ -70,6 +72,8 @@ def main():
         gs.TMATMUL_HEAD_MATH = args.head_math
     if args.tn_math is not None:
         dense.TN_MATH = args.tn_math
+    if args.hybrid_max_cols is not None:
+        gs.HYBRID_MAX_COLS = args.hybrid_max_cols
     cfg = CONFIGS[args.config]
     dev = torch.device("cuda:0")
     if args.inline_weight_grads:
@@ -129,6 +133,7 @@ def main():
            "legacy_stride": args.legacy_stride, "nt_math": dense.NT_MATH,
            "theano_backward": args.theano_backward, "side_priority": dense.SIDE_STREAM_PRIORITY,
            "head_math": gs.TMATMUL_HEAD_MATH or dense.TN_MATH, "tn_math": dense.TN_MATH,
+           "hybrid_max_cols": gs.HYBRID_MAX_COLS,
            "data_gen_s": round(t_gen, 1)}
     print(json.dumps(rec), flush=True)
 
