@@ -1,10 +1,13 @@
 """Host-side layout rule of the dense operands (sparse.row_stride / empty_dense's row stride):
 16-B aligned rows whose gathered K floats span the fewest 128-B lines."""
 import math
+import os
 
 import pytest
 
 from graphconvgeo_amd.sparse import row_stride
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def lines(start: int, nbytes: int) -> int:
@@ -47,3 +50,20 @@ def test_row_stride_known_values():
     assert row_stride(129) == 132 and row_stride(258) == 260
     assert row_stride(500) == 512    # the reference's default hidden size (tensormain.py:82)
     assert math.gcd(4 * row_stride(300), 128) == 64
+
+
+def test_package_sets_graph_branch_streams_before_hip_starts():
+    """The HIP runtime reads DEBUG_HIP_FORCE_GRAPH_QUEUES once, when it initialises: importing
+    the package (in a fresh interpreter, no HIP yet) sets the default of 8, and an explicit
+    setting wins (profiles/r06/graph_queues_ab*.txt)."""
+    import subprocess
+    import sys
+    code = "import os, graphconvgeo_amd; print(os.environ['DEBUG_HIP_FORCE_GRAPH_QUEUES'])"
+    env = {k: v for k, v in os.environ.items() if k != "DEBUG_HIP_FORCE_GRAPH_QUEUES"}
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         cwd=ROOT, check=True).stdout.strip()
+    assert out == "8"
+    env["DEBUG_HIP_FORCE_GRAPH_QUEUES"] = "2"
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                         cwd=ROOT, check=True).stdout.strip()
+    assert out == "2"
